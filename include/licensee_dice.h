@@ -1,0 +1,135 @@
+/*
+ * licensee_dice.h -- C-ABI of the MI355X-native Dice scorer (gfx950 / HIP).
+ *
+ * Drop-in boundary for licensee's Dice matching hot path. The reference has no FFI for
+ * this path (it is pure Ruby); every entry point below replaces a Ruby method and is what
+ * a Ruby FFI binding attaches. Citations are to /root/reference:
+ *
+ *   dice_create / dice_destroy      replace the process-wide memoized template corpus:
+ *                                   License.all(hidden: true, psuedo: false)   lib/licensee/license.rb:20-36
+ *                                   + per-template wordset_fieldless / fields_normalized(_set) /
+ *                                   length / spdx_alt_segments   lib/licensee/content_helper.rb:108-117,323-335
+ *                                   lib/licensee/license.rb:273-283
+ *   dice_match                      Dice#match + #confidence + the score loop of
+ *                                   #matches_by_similarity        lib/licensee/matchers/dice.rb:8-14,34-53
+ *                                   over License#similarity        lib/licensee/content_helper.rb:128-133,337-347
+ *                                   with the CC filter of #potential_matches  dice.rb:23-31
+ *   dice_similarity_matrix          Dice#matches_by_similarity / #licenses_by_similarity (full N x T
+ *                                   scores + sorted top-k, no threshold cut)  dice.rb:34-41;
+ *                                   also `licensee detect` "closest licenses" lib/licensee/commands/detect.rb:96-106
+ *   dice_batch_*                    device-resident batch variants of the two calls above
+ *   dice_last_error                 replaces the Ruby exceptions of the path (license.rb:258,
+ *                                   content_helper.rb:230,310) with status codes + message
+ *
+ * Conventions
+ *   - Caller owns every host buffer; the library owns all device memory inside a ctx/batch.
+ *   - Every call returns DICE_OK (0) or a negative DICE_E_* code; dice_last_error() gives a
+ *     thread-local message for the last failing call on this thread.
+ *   - One ctx per host thread (no internal locking). Host-buffer calls are synchronous.
+ *   - `stream` arguments are hipStream_t passed as void* (NULL = the ctx's own stream).
+ *   - Bitsets: bit v of a word-set bitset is word-id v of the template vocabulary
+ *     (word v lives in uint64 word v/64, bit v%64). Vocabulary = union of the templates'
+ *     wordset_fieldless; words outside it cannot overlap and only count in |W_F|.
+ *   - Results are bit-exact with the reference: overlap counts are exact integers, scores are
+ *     IEEE-754 double (overlap*200.0)/denominator with Ruby's Integer floor division inside
+ *     the denominator. Exact score ties (parity-unpinned in the reference, whose sort is not
+ *     stable) resolve to the template LATER in key order.
+ */
+#ifndef LICENSEE_DICE_H
+#define LICENSEE_DICE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DICE_OK 0
+#define DICE_E_ARG (-1)       /* invalid argument / shape */
+#define DICE_E_DEVICE (-2)    /* HIP runtime error or no usable gfx950 device */
+#define DICE_E_NOMEM (-3)     /* host or device allocation failed */
+#define DICE_E_STATE (-4)     /* call not valid in the current state */
+
+#define DICE_TOPK_MAX 16
+
+typedef struct dice_ctx dice_ctx;
+typedef struct dice_batch dice_batch;
+
+/* One entry per template, in License.all(hidden: true, psuedo: false) key order. */
+typedef struct dice_templates {
+    int32_t n_templates;            /* T (>= 1)                                              */
+    int32_t n_vocab;                /* V, bits per bitset (>= 1)                              */
+    const uint64_t *lf_bits;        /* [T][dice_words64(V)]: wordset_fieldless (Lf) bitsets  */
+    const uint32_t *lf_size;        /* [T] |Lf|            (content_helper.rb:130)            */
+    const uint32_t *fields_set_size;/* [T] |fields_normalized_set| (content_helper.rb:131)    */
+    const int32_t *length_slack;    /* [T] 5*max(fields_normalized.size, spdx_alt_segments)  */
+                                    /*     (content_helper.rb:345); < 0 selects the simple   */
+                                    /*     delta used when self is not a License (:343)      */
+    const int32_t *length;          /* [T] content_normalized.length (characters)           */
+    const uint8_t *is_cc;           /* [T] creative_commons? (license.rb:209-212)             */
+} dice_templates;
+
+/* A batch of candidate files (host memory). */
+typedef struct dice_files {
+    int64_t n_files;
+    const uint64_t *bits;           /* [n][dice_words64(V)] row-major wordset bitsets        */
+    const uint32_t *wordset_size;   /* [n] |W_F|: all distinct words, in or out of vocabulary */
+    const int32_t *length;          /* [n] content_normalized.length (characters)            */
+    const uint8_t *cc_false_positive; /* [n] potential_false_positive? (license_file.rb:80-82) */
+} dice_files;
+
+/* Number of uint64 words per bitset for a vocabulary of n_vocab words. */
+int32_t dice_words64(int32_t n_vocab);
+
+/* Upload a template corpus to `device` (HIP ordinal). Selects the kernel for the corpus
+ * (template-specialized sparse program for T <= 64, dense tiled otherwise). */
+int dice_create(const dice_templates *templates, int32_t device, dice_ctx **out);
+void dice_destroy(dice_ctx *ctx);
+
+/* Introspection: T, V, kernel kind (0 = dense, 1 = sparse program), program entries. */
+int dice_ctx_info(const dice_ctx *ctx, int32_t *n_templates, int32_t *n_vocab,
+                  int32_t *kernel_kind, int32_t *program_entries);
+
+/* Dice#match / #confidence for every file, synchronous, host buffers.
+ *   best[i]    index of the matched template, or -1 (Dice#match nil) when the top
+ *              score is below `threshold` or every template is CC-filtered;
+ *   overlap[i] |Lf ∩ W_F| of the top-ranked template (0 if none);
+ *   score[i]   similarity of the top-ranked template (0.0 if none) -- equals
+ *              Dice#confidence when best[i] >= 0.
+ * Any of the three output pointers may be NULL. */
+int dice_match(dice_ctx *ctx, const dice_files *files, double threshold,
+               int32_t *best, uint32_t *overlap, double *score);
+
+/* Full N x T similarity matrix + per-file top-k (Dice#matches_by_similarity order).
+ *   overlap/score: [n][T] row-major, every template (CC filter NOT applied), may be NULL;
+ *   topk_index/topk_score: [n][k] best-first among potential_matches (CC filter applied),
+ *   -1 / -1.0 padding; k in [0, DICE_TOPK_MAX]. */
+int dice_similarity_matrix(dice_ctx *ctx, const dice_files *files,
+                           uint32_t *overlap, double *score,
+                           int32_t k, int32_t *topk_index, double *topk_score);
+
+/* ---- device-resident batches (inputs and results stay in HBM) ---------------------- */
+int dice_batch_create(dice_ctx *ctx, int64_t capacity, dice_batch **out);
+void dice_batch_destroy(dice_batch *batch);
+/* H2D copy + on-device repack of host files into the kernel's tile layout. */
+int dice_batch_upload(dice_batch *batch, const dice_files *files, void *stream);
+/* Kernel-only scoring of the resident batch (asynchronous on `stream`). */
+int dice_batch_match(dice_batch *batch, double threshold, void *stream);
+int dice_batch_matrix(dice_batch *batch, int32_t k, void *stream);
+/* D2H of results (synchronizes `stream`); NULL outputs are skipped. */
+int dice_batch_download_match(dice_batch *batch, int32_t *best, uint32_t *overlap,
+                              double *score, void *stream);
+int dice_batch_download_matrix(dice_batch *batch, uint32_t *overlap, double *score,
+                               int32_t *topk_index, double *topk_score, void *stream);
+/* Device pointers of the match results (int32 best, uint32 overlap, double score). */
+int dice_batch_result_ptrs(dice_batch *batch, void **best, void **overlap, void **score);
+/* Bytes of the resident tile layout per file (the kernel's algorithmic input stream). */
+int64_t dice_batch_bytes_per_file(const dice_batch *batch);
+
+const char *dice_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LICENSEE_DICE_H */

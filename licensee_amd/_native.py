@@ -1,0 +1,246 @@
+"""ctypes binding of the C-ABI in include/licensee_dice.h (liblicensee_dice.so).
+
+This is the product's only scoring path: if the HIP library is missing or no gfx950
+device is usable, calls raise -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib')
+LIB_PATH = os.path.join(LIB_DIR, 'liblicensee_dice.so')
+
+DICE_OK = 0
+DICE_TOPK_MAX = 16
+
+EXPORTED_SYMBOLS = (
+    'dice_words64', 'dice_create', 'dice_destroy', 'dice_ctx_info', 'dice_match',
+    'dice_similarity_matrix', 'dice_batch_create', 'dice_batch_destroy', 'dice_batch_upload',
+    'dice_batch_match', 'dice_batch_matrix', 'dice_batch_download_match',
+    'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
+    'dice_last_error',
+)
+
+
+class DiceError(RuntimeError):
+    pass
+
+
+class _Templates(ctypes.Structure):
+    _fields_ = [('n_templates', ctypes.c_int32), ('n_vocab', ctypes.c_int32),
+                ('lf_bits', ctypes.c_void_p), ('lf_size', ctypes.c_void_p),
+                ('fields_set_size', ctypes.c_void_p), ('length_slack', ctypes.c_void_p),
+                ('length', ctypes.c_void_p), ('is_cc', ctypes.c_void_p)]
+
+
+class _Files(ctypes.Structure):
+    _fields_ = [('n_files', ctypes.c_int64), ('bits', ctypes.c_void_p),
+                ('wordset_size', ctypes.c_void_p), ('length', ctypes.c_void_p),
+                ('cc_false_positive', ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load liblicensee_dice.so (raises if it was not built -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DiceError(f'{path} is missing: build it with `python -c "import __graft_entry__ as g; g.build()"`')
+    lib = ctypes.CDLL(path)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        'dice_words64': (i32, [i32]),
+        'dice_create': (ctypes.c_int, [ctypes.POINTER(_Templates), i32, ctypes.POINTER(vp)]),
+        'dice_destroy': (None, [vp]),
+        'dice_ctx_info': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        'dice_match': (ctypes.c_int, [vp, ctypes.POINTER(_Files), ctypes.c_double, vp, vp, vp]),
+        'dice_similarity_matrix': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp, vp, i32, vp, vp]),
+        'dice_batch_create': (ctypes.c_int, [vp, i64, ctypes.POINTER(vp)]),
+        'dice_batch_destroy': (None, [vp]),
+        'dice_batch_upload': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp]),
+        'dice_batch_match': (ctypes.c_int, [vp, ctypes.c_double, vp]),
+        'dice_batch_matrix': (ctypes.c_int, [vp, i32, vp]),
+        'dice_batch_download_match': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        'dice_batch_download_matrix': (ctypes.c_int, [vp, vp, vp, vp, vp, vp]),
+        'dice_batch_result_ptrs': (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+        'dice_batch_bytes_per_file': (i64, [vp]),
+        'dice_last_error': (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != DICE_OK:
+        msg = load_library().dice_last_error().decode('utf-8', 'replace')
+        raise DiceError(f'dice error {rc}: {msg}')
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+def words64(n_vocab: int) -> int:
+    return (n_vocab + 63) // 64
+
+
+@dataclass
+class FileBatch:
+    """Interned candidate files (host memory), the layout of ``dice_files``."""
+    bits: np.ndarray            # [n, words64(V)] uint64
+    wordset_size: np.ndarray    # [n] uint32
+    length: np.ndarray          # [n] int32
+    cc_false_positive: np.ndarray  # [n] uint8
+
+    def __post_init__(self):
+        self.bits = np.ascontiguousarray(self.bits, dtype=np.uint64)
+        self.wordset_size = np.ascontiguousarray(self.wordset_size, dtype=np.uint32)
+        self.length = np.ascontiguousarray(self.length, dtype=np.int32)
+        self.cc_false_positive = np.ascontiguousarray(self.cc_false_positive, dtype=np.uint8)
+        n = self.bits.shape[0]
+        if not (self.wordset_size.shape == self.length.shape == self.cc_false_positive.shape == (n,)):
+            raise ValueError('inconsistent FileBatch shapes')
+
+    @property
+    def n(self) -> int:
+        return self.bits.shape[0]
+
+    def _struct(self) -> _Files:
+        return _Files(self.n, _ptr(self.bits), _ptr(self.wordset_size), _ptr(self.length),
+                      _ptr(self.cc_false_positive))
+
+
+class Scorer:
+    """Owns a ``dice_ctx``: one template corpus resident on one gfx950 device."""
+
+    def __init__(self, lf_bits: np.ndarray, lf_size, fields_set_size, length_slack, length, is_cc,
+                 n_vocab: int, device: int = 0):
+        lib = load_library()
+        self._keep = [np.ascontiguousarray(lf_bits, dtype=np.uint64),
+                      np.ascontiguousarray(lf_size, dtype=np.uint32),
+                      np.ascontiguousarray(fields_set_size, dtype=np.uint32),
+                      np.ascontiguousarray(length_slack, dtype=np.int32),
+                      np.ascontiguousarray(length, dtype=np.int32),
+                      np.ascontiguousarray(is_cc, dtype=np.uint8)]
+        T = self._keep[1].shape[0]
+        if self._keep[0].shape != (T, words64(n_vocab)):
+            raise ValueError('lf_bits must be [T, words64(V)]')
+        self.n_templates, self.n_vocab, self.device = T, n_vocab, device
+        tpl = _Templates(T, n_vocab, *[_ptr(a) for a in self._keep])
+        ctx = ctypes.c_void_p()
+        _check(lib.dice_create(ctypes.byref(tpl), device, ctypes.byref(ctx)))
+        self._ctx = ctx
+
+    def close(self):
+        if getattr(self, '_ctx', None):
+            load_library().dice_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> Tuple[int, int, int, int]:
+        vals = [ctypes.c_int32() for _ in range(4)]
+        _check(load_library().dice_ctx_info(self._ctx, *[ctypes.byref(v) for v in vals]))
+        return tuple(v.value for v in vals)
+
+    def match(self, files: FileBatch, threshold: float):
+        n = files.n
+        best = np.empty(n, np.int32)
+        ov = np.empty(n, np.uint32)
+        score = np.empty(n, np.float64)
+        if n:
+            st = files._struct()
+            _check(load_library().dice_match(self._ctx, ctypes.byref(st), float(threshold),
+                                             _ptr(best), _ptr(ov), _ptr(score)))
+        return best, ov, score
+
+    def matrix(self, files: FileBatch, k: int = 0):
+        n, T = files.n, self.n_templates
+        ov = np.empty((n, T), np.uint32)
+        score = np.empty((n, T), np.float64)
+        tki = np.empty((n, max(k, 0)), np.int32)
+        tks = np.empty((n, max(k, 0)), np.float64)
+        if n:
+            st = files._struct()
+            _check(load_library().dice_similarity_matrix(self._ctx, ctypes.byref(st), _ptr(ov), _ptr(score), k,
+                                                         _ptr(tki) if k else None, _ptr(tks) if k else None))
+        return ov, score, tki, tks
+
+    def batch(self, capacity: int) -> 'DeviceBatch':
+        return DeviceBatch(self, capacity)
+
+
+class DeviceBatch:
+    """A device-resident batch (``dice_batch``): upload once, score many times."""
+
+    def __init__(self, scorer: Scorer, capacity: int):
+        self.scorer = scorer
+        b = ctypes.c_void_p()
+        _check(load_library().dice_batch_create(scorer._ctx, int(capacity), ctypes.byref(b)))
+        self._b = b
+        self.n = 0
+
+    def close(self):
+        if getattr(self, '_b', None):
+            load_library().dice_batch_destroy(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, files: FileBatch, stream: int = 0):
+        st = files._struct()
+        _check(load_library().dice_batch_upload(self._b, ctypes.byref(st), stream or None))
+        self.n = files.n
+
+    def match(self, threshold: float, stream: int = 0):
+        _check(load_library().dice_batch_match(self._b, float(threshold), stream or None))
+
+    def matrix(self, k: int, stream: int = 0):
+        _check(load_library().dice_batch_matrix(self._b, int(k), stream or None))
+
+    def download_match(self, stream: int = 0):
+        n = self.n
+        best = np.empty(n, np.int32)
+        ov = np.empty(n, np.uint32)
+        score = np.empty(n, np.float64)
+        _check(load_library().dice_batch_download_match(self._b, _ptr(best), _ptr(ov), _ptr(score), stream or None))
+        return best, ov, score
+
+    def download_matrix(self, k: int, stream: int = 0):
+        n, T = self.n, self.scorer.n_templates
+        ov = np.empty((n, T), np.uint32)
+        score = np.empty((n, T), np.float64)
+        tki = np.empty((n, max(k, 1)), np.int32)
+        tks = np.empty((n, max(k, 1)), np.float64)
+        _check(load_library().dice_batch_download_matrix(self._b, _ptr(ov), _ptr(score),
+                                                         _ptr(tki) if k else None, _ptr(tks) if k else None,
+                                                         stream or None))
+        return ov, score, tki[:, :k], tks[:, :k]
+
+    def result_ptrs(self):
+        p = [ctypes.c_void_p() for _ in range(3)]
+        _check(load_library().dice_batch_result_ptrs(self._b, *[ctypes.byref(x) for x in p]))
+        return tuple(x.value for x in p)
+
+    def bytes_per_file(self) -> int:
+        return int(load_library().dice_batch_bytes_per_file(self._b))

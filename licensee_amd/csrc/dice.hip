@@ -1,0 +1,576 @@
+// MI355X (gfx950) Dice scorer: kernels + C-ABI (include/licensee_dice.h).
+//
+// Hot path replaced: lib/licensee/matchers/dice.rb:34-53 looping
+// License#similarity (lib/licensee/content_helper.rb:128-133,337-347) over every template.
+//
+// Device layout (HBM):
+//   files   : tile layout [n_tiles][Wq][64 lanes] of uint4 -- one wave owns a tile of 64 files,
+//             lane l holds file (tile*64 + l); quad q carries vocab bits [128q, 128q+128).
+//             Every wave-instruction loads 1 KiB contiguous (global_load_dwordx4, coalesced).
+//   scalars : |W_F| (u32), len_F (i32), cc flag (u8), SoA, padded to n_tiles*64.
+//   tpl     : [Wq][Tpad] uint4 template quads (uniform -> scalar loads into SGPRs) + TplConst.
+//   results : best (i32), overlap (u32), score (f64) per file, SoA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/licensee_dice.h"
+#include "dice_common.h"
+#include "dice_program.h"
+
+using namespace dice;
+
+// ---------------------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------------------
+
+// Row-major uint64 bitsets [n][W64] -> tile layout [n_tiles][Wq][64] uint4 (zero padded).
+__global__ __launch_bounds__(256) void dice_pack_tiles(const uint64_t* __restrict__ rows, int64_t n,
+                                                       int32_t w64, int32_t wq,
+                                                       uint4* __restrict__ tiles, int64_t n_tiles) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = n_tiles * wq * kWave;
+    if (gid >= total) return;
+    const int lane = (int)(gid & (kWave - 1));
+    const int64_t tq = gid >> 6;
+    const int q = (int)(tq % wq);
+    const int64_t tile = tq / wq;
+    const int64_t file = tile * kWave + lane;
+    uint64_t a = 0, b = 0;
+    if (file < n) {
+        const uint64_t* r = rows + file * w64;
+        if (2 * q < w64) a = r[2 * q];
+        if (2 * q + 1 < w64) b = r[2 * q + 1];
+    }
+    tiles[gid] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+
+__device__ __forceinline__ uint32_t popc_and4(uint4 f, uint4 m) {
+    return __popc(f.x & m.x) + __popc(f.y & m.y) + __popc(f.z & m.z) + __popc(f.w & m.w);
+}
+
+// Dense scorer: any T, any V. Templates are uniform across the wave, so the compiler keeps
+// them on the scalar path (s_load -> SGPR operand of v_and_b32); file quads stream through
+// VGPRs. TT templates are accumulated per pass (compile-time register array).
+template <int TT>
+__global__ __launch_bounds__(256) void dice_dense_match(
+    const uint4* __restrict__ files, int64_t n, int32_t wq, const uint4* __restrict__ tq,
+    const int4* __restrict__ tc, int32_t T, int32_t tpad, const uint32_t* __restrict__ wf,
+    const int32_t* __restrict__ lenf, const uint8_t* __restrict__ ccfp, double thr,
+    int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    if (tile * kWave >= n) return;  // wave-uniform
+    const int64_t file = tile * kWave + lane;
+    const uint4* fp = files + tile * (int64_t)wq * kWave + lane;
+    const uint32_t my_wf = wf[file];
+    const int32_t my_len = lenf[file];
+    const bool my_cc = ccfp[file] != 0;
+
+    Best best;
+    best.init();
+    for (int t0 = 0; t0 < T; t0 += TT) {
+        uint32_t acc[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) acc[j] = 0;
+        const uint4* mrow = tq + t0;
+        for (int q = 0; q < wq; ++q) {
+            const uint4 f = fp[(int64_t)q * kWave];
+#pragma unroll
+            for (int j = 0; j < TT; ++j) acc[j] += popc_and4(f, mrow[j]);
+            mrow += tpad;
+        }
+#pragma unroll
+        for (int j = 0; j < TT; ++j) {
+            const int t = t0 + j;
+            if (t < T) {
+                const int4 c = tc[t];
+                if (!(c.w && my_cc)) best.offer(t, acc[j], dice_den(c, my_wf, my_len));
+            }
+        }
+    }
+    if (file < n) {
+        const double s = best.idx >= 0 ? dice_score(best.ov, best.den) : 0.0;
+        best_out[file] = (best.idx >= 0 && s >= thr) ? best.idx : -1;
+        ov_out[file] = best.ov;
+        score_out[file] = s;
+    }
+}
+
+// Top-k insertion (best-first, later template first among exact ties) over registers.
+struct TopK {
+    int32_t idx[kTopKMax];
+    uint32_t ov[kTopKMax];
+    int32_t den[kTopKMax];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < kTopKMax; ++j) { idx[j] = -1; ov[j] = 0; den[j] = 1; }
+    }
+    __device__ __forceinline__ void offer(int k, int32_t t, uint32_t o, int32_t d) {
+        bool carrying = true, placed = false;
+        int32_t ci = t; uint32_t co = o; int32_t cd = d;
+#pragma unroll
+        for (int j = 0; j < kTopKMax; ++j) {
+            if (j < k && carrying) {
+                if (idx[j] < 0) {
+                    idx[j] = ci; ov[j] = co; den[j] = cd; carrying = false;
+                } else if (placed || dice_ge(co, cd, ov[j], den[j])) {
+                    const int32_t ti = idx[j]; const uint32_t to = ov[j]; const int32_t td = den[j];
+                    idx[j] = ci; ov[j] = co; den[j] = cd;
+                    ci = ti; co = to; cd = td; placed = true;
+                }
+            }
+        }
+    }
+};
+
+template <int TT>
+__global__ __launch_bounds__(256) void dice_dense_matrix(
+    const uint4* __restrict__ files, int64_t n, int32_t wq, const uint4* __restrict__ tq,
+    const int4* __restrict__ tc, int32_t T, int32_t tpad, const uint32_t* __restrict__ wf,
+    const int32_t* __restrict__ lenf, const uint8_t* __restrict__ ccfp, int32_t k,
+    uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t* __restrict__ topk_idx,
+    double* __restrict__ topk_score) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    if (tile * kWave >= n) return;
+    const int64_t file = tile * kWave + lane;
+    const bool valid = file < n;
+    const uint4* fp = files + tile * (int64_t)wq * kWave + lane;
+    const uint32_t my_wf = wf[file];
+    const int32_t my_len = lenf[file];
+    const bool my_cc = ccfp[file] != 0;
+
+    TopK top;
+    top.init();
+    for (int t0 = 0; t0 < T; t0 += TT) {
+        uint32_t acc[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) acc[j] = 0;
+        const uint4* mrow = tq + t0;
+        for (int q = 0; q < wq; ++q) {
+            const uint4 f = fp[(int64_t)q * kWave];
+#pragma unroll
+            for (int j = 0; j < TT; ++j) acc[j] += popc_and4(f, mrow[j]);
+            mrow += tpad;
+        }
+#pragma unroll
+        for (int j = 0; j < TT; ++j) {
+            const int t = t0 + j;
+            if (t < T) {
+                const int4 c = tc[t];
+                const int32_t den = dice_den(c, my_wf, my_len);
+                if (valid) {
+                    if (ov_out) ov_out[file * T + t] = acc[j];
+                    if (score_out) score_out[file * T + t] = dice_score(acc[j], den);
+                }
+                if (!(c.w && my_cc)) top.offer(k, t, acc[j], den);
+            }
+        }
+    }
+    if (valid && topk_idx) {
+#pragma unroll
+        for (int j = 0; j < kTopKMax; ++j) {
+            if (j < k) {
+                topk_idx[file * k + j] = top.idx[j];
+                topk_score[file * k + j] = top.idx[j] >= 0 ? dice_score(top.ov[j], top.den[j]) : -1.0;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(DICE_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+constexpr int kTT = 48;        // templates per dense pass
+constexpr int kBlock = 256;    // 4 waves, one 64-file tile each
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <class T>
+int dalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) return fail(DICE_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return DICE_OK;
+}
+
+}  // namespace
+
+struct dice_ctx {
+    int device = 0;
+    int32_t T = 0, V = 0, w64 = 0, wq = 0, tpad = 0;
+    hipStream_t stream = nullptr;
+    uint4* d_tq = nullptr;  // [wq][tpad]
+    int4* d_tc = nullptr;   // [tpad]
+    int32_t kind = 0;       // 0 dense, 1 sparse program
+    dice::Program prog;     // sparse program (kind 1)
+    hipModule_t module = nullptr;
+    hipFunction_t prog_match = nullptr;
+    hipFunction_t prog_matrix = nullptr;
+    dice_batch* scratch = nullptr;  // reused by the host-buffer calls
+};
+
+struct dice_batch {
+    dice_ctx* ctx = nullptr;
+    int64_t capacity = 0, n = 0, n_tiles_cap = 0;
+    uint64_t* d_rows = nullptr;     // staging [capacity][w64]
+    uint4* d_tiles = nullptr;       // [n_tiles][wq][64]
+    uint32_t* d_wf = nullptr;
+    int32_t* d_len = nullptr;
+    uint8_t* d_cc = nullptr;
+    int32_t* d_best = nullptr;
+    uint32_t* d_ov = nullptr;
+    double* d_score = nullptr;
+    // matrix results (lazily allocated)
+    int64_t mat_cap = 0;
+    int32_t mat_k = 0;
+    int32_t k_used = 0;
+    uint32_t* d_mov = nullptr;
+    double* d_mscore = nullptr;
+    int32_t* d_tki = nullptr;
+    double* d_tks = nullptr;
+};
+
+namespace dice {
+// Stage 1: dense kernel for every corpus (the sparse program is selected in a later stage).
+int program_setup(dice_ctx* c, const dice_templates*) { c->kind = 0; return DICE_OK; }
+int program_launch_match(dice_ctx*, dice_batch*, double, hipStream_t) { return fail(DICE_E_STATE, "no program"); }
+int program_launch_matrix(dice_ctx*, dice_batch*, int32_t, hipStream_t) { return fail(DICE_E_STATE, "no program"); }
+}  // namespace dice
+
+static hipStream_t pick_stream(dice_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+
+extern "C" {
+
+int32_t dice_words64(int32_t n_vocab) { return n_vocab <= 0 ? 0 : (n_vocab + 63) / 64; }
+
+const char* dice_last_error(void) { return g_err.c_str(); }
+
+static void ctx_free(dice_ctx* c) {
+    if (!c) return;
+    if (c->scratch) dice_batch_destroy(c->scratch);
+    if (c->d_tq) (void)hipFree(c->d_tq);
+    if (c->d_tc) (void)hipFree(c->d_tc);
+    if (c->module) (void)hipModuleUnload(c->module);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
+    if (!out) return fail(DICE_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (!t || t->n_templates < 1 || t->n_vocab < 1 || !t->lf_bits || !t->lf_size ||
+        !t->fields_set_size || !t->length_slack || !t->length || !t->is_cc)
+        return fail(DICE_E_ARG, "invalid dice_templates");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(DICE_E_DEVICE, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(DICE_E_DEVICE, std::string("requires gfx950, found ") + prop.gcnArchName);
+    DeviceGuard g(device);
+    if (!g.ok) return fail(DICE_E_DEVICE, "hipSetDevice failed");
+
+    dice_ctx* c = new (std::nothrow) dice_ctx();
+    if (!c) return fail(DICE_E_NOMEM, "ctx alloc");
+    c->device = device;
+    c->T = t->n_templates;
+    c->V = t->n_vocab;
+    c->w64 = dice_words64(t->n_vocab);
+    c->wq = (c->w64 + 1) / 2;
+    c->tpad = ((c->T + kTT - 1) / kTT) * kTT;
+    int rc;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        ctx_free(c);
+        return fail(DICE_E_DEVICE, "hipStreamCreate failed");
+    }
+    std::vector<uint4> hq((size_t)c->wq * c->tpad, make_uint4(0, 0, 0, 0));
+    std::vector<int4> hc((size_t)c->tpad, make_int4(0, 0, 0, 0));
+    for (int32_t i = 0; i < c->T; ++i) {
+        const uint64_t* r = t->lf_bits + (size_t)i * c->w64;
+        for (int32_t q = 0; q < c->wq; ++q) {
+            uint64_t a = r[2 * q], b = (2 * q + 1 < c->w64) ? r[2 * q + 1] : 0;
+            hq[(size_t)q * c->tpad + i] =
+                make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+        }
+        hc[i] = make_int4((int32_t)t->lf_size[i] - (int32_t)t->fields_set_size[i], t->length_slack[i],
+                          t->length[i], t->is_cc[i] ? 1 : 0);
+    }
+    if ((rc = dalloc(&c->d_tq, hq.size())) || (rc = dalloc(&c->d_tc, hc.size()))) {
+        ctx_free(c);
+        return rc;
+    }
+    if (hipMemcpy(c->d_tq, hq.data(), hq.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_tc, hc.data(), hc.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess) {
+        ctx_free(c);
+        return fail(DICE_E_DEVICE, "template upload failed");
+    }
+    // Sparse-program kernel for small corpora (see dice_program.h).
+    rc = dice::program_setup(c, t);
+    if (rc != DICE_OK) {
+        ctx_free(c);
+        return rc;
+    }
+    *out = c;
+    return DICE_OK;
+}
+
+void dice_destroy(dice_ctx* ctx) {
+    if (!ctx) return;
+    DeviceGuard g(ctx->device);
+    ctx_free(ctx);
+}
+
+int dice_ctx_info(const dice_ctx* ctx, int32_t* T, int32_t* V, int32_t* kind, int32_t* entries) {
+    if (!ctx) return fail(DICE_E_ARG, "ctx is NULL");
+    if (T) *T = ctx->T;
+    if (V) *V = ctx->V;
+    if (kind) *kind = ctx->kind;
+    if (entries) *entries = (int32_t)ctx->prog.entries();
+    return DICE_OK;
+}
+
+void dice_batch_destroy(dice_batch* b) {
+    if (!b) return;
+    DeviceGuard g(b->ctx->device);
+    void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf, b->d_len, b->d_cc, b->d_best,
+                    b->d_ov,   b->d_score, b->d_mov, b->d_mscore, b->d_tki, b->d_tks};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete b;
+}
+
+int dice_batch_create(dice_ctx* ctx, int64_t capacity, dice_batch** out) {
+    if (!ctx || !out || capacity < 1) return fail(DICE_E_ARG, "invalid batch arguments");
+    *out = nullptr;
+    DeviceGuard g(ctx->device);
+    dice_batch* b = new (std::nothrow) dice_batch();
+    if (!b) return fail(DICE_E_NOMEM, "batch alloc");
+    b->ctx = ctx;
+    b->capacity = capacity;
+    b->n_tiles_cap = (capacity + kWave - 1) / kWave;
+    const int64_t npad = b->n_tiles_cap * kWave;
+    int rc;
+    if ((rc = dalloc(&b->d_rows, (size_t)capacity * ctx->w64)) ||
+        (rc = dalloc(&b->d_tiles, (size_t)b->n_tiles_cap * ctx->wq * kWave)) ||
+        (rc = dalloc(&b->d_wf, npad)) || (rc = dalloc(&b->d_len, npad)) || (rc = dalloc(&b->d_cc, npad)) ||
+        (rc = dalloc(&b->d_best, npad)) || (rc = dalloc(&b->d_ov, npad)) || (rc = dalloc(&b->d_score, npad))) {
+        dice_batch_destroy(b);
+        return rc;
+    }
+    *out = b;
+    return DICE_OK;
+}
+
+int64_t dice_batch_bytes_per_file(const dice_batch* b) {
+    if (!b) return -1;
+    return (int64_t)b->ctx->wq * 16;
+}
+
+int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
+    if (!b || !f) return fail(DICE_E_ARG, "NULL batch/files");
+    dice_ctx* c = b->ctx;
+    if (f->n_files < 0 || f->n_files > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
+    if (f->n_files > 0 && (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive))
+        return fail(DICE_E_ARG, "NULL file arrays");
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    const int64_t n = f->n_files;
+    b->n = n;
+    if (n == 0) return DICE_OK;
+    const int64_t n_tiles = (n + kWave - 1) / kWave;
+    const int64_t npad = n_tiles * kWave;
+    HIP_TRY(hipMemcpyAsync(b->d_rows, f->bits, (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_wf, f->wordset_size, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_len, f->length, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_cc, f->cc_false_positive, (size_t)n, hipMemcpyHostToDevice, s));
+    if (npad > n) {
+        HIP_TRY(hipMemsetAsync(b->d_wf + n, 0, (size_t)(npad - n) * 4, s));
+        HIP_TRY(hipMemsetAsync(b->d_len + n, 0, (size_t)(npad - n) * 4, s));
+        HIP_TRY(hipMemsetAsync(b->d_cc + n, 0, (size_t)(npad - n), s));
+    }
+    const int64_t total = n_tiles * c->wq * kWave;
+    const unsigned grid = (unsigned)((total + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(dice_pack_tiles, dim3(grid), dim3(kBlock), 0, s, b->d_rows, n, c->w64, c->wq,
+                       b->d_tiles, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return DICE_OK;
+}
+
+int dice_batch_match(dice_batch* b, double thr, void* stream) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    dice_ctx* c = b->ctx;
+    if (b->n == 0) return DICE_OK;
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    const int64_t n_tiles = (b->n + kWave - 1) / kWave;
+    const unsigned grid = (unsigned)((n_tiles + (kBlock / kWave) - 1) / (kBlock / kWave));
+    if (c->kind == 1) {
+        int rc = dice::program_launch_match(c, b, thr, s);
+        if (rc != DICE_OK) return rc;
+    } else {
+        hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
+                           c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
+                           b->d_ov, b->d_score);
+    }
+    HIP_TRY(hipGetLastError());
+    return DICE_OK;
+}
+
+static int ensure_matrix(dice_batch* b, int32_t k) {
+    dice_ctx* c = b->ctx;
+    if (b->mat_cap >= b->capacity && b->mat_k >= k && b->d_mov) return DICE_OK;
+    void* ptrs[] = {b->d_mov, b->d_mscore, b->d_tki, b->d_tks};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    b->d_mov = nullptr; b->d_mscore = nullptr; b->d_tki = nullptr; b->d_tks = nullptr;
+    int rc;
+    const int32_t kk = std::max<int32_t>(k, 1);
+    if ((rc = dalloc(&b->d_mov, (size_t)b->capacity * c->T)) ||
+        (rc = dalloc(&b->d_mscore, (size_t)b->capacity * c->T)) ||
+        (rc = dalloc(&b->d_tki, (size_t)b->capacity * kk)) || (rc = dalloc(&b->d_tks, (size_t)b->capacity * kk)))
+        return rc;
+    b->mat_cap = b->capacity;
+    b->mat_k = kk;
+    return DICE_OK;
+}
+
+int dice_batch_matrix(dice_batch* b, int32_t k, void* stream) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    if (k < 0 || k > DICE_TOPK_MAX) return fail(DICE_E_ARG, "k out of range");
+    dice_ctx* c = b->ctx;
+    if (b->n == 0) return DICE_OK;
+    DeviceGuard g(c->device);
+    int rc = ensure_matrix(b, k);
+    if (rc) return rc;
+    b->k_used = k;
+    hipStream_t s = pick_stream(c, stream);
+    const int64_t n_tiles = (b->n + kWave - 1) / kWave;
+    const unsigned grid = (unsigned)((n_tiles + (kBlock / kWave) - 1) / (kBlock / kWave));
+    if (c->kind == 1) {
+        rc = dice::program_launch_matrix(c, b, k, s);
+        if (rc != DICE_OK) return rc;
+    } else {
+        hipLaunchKernelGGL(dice_dense_matrix<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
+                           c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, k, b->d_mov,
+                           b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks);
+    }
+    HIP_TRY(hipGetLastError());
+    return DICE_OK;
+}
+
+int dice_batch_download_match(dice_batch* b, int32_t* best, uint32_t* ov, double* score, void* stream) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    dice_ctx* c = b->ctx;
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    const size_t n = (size_t)b->n;
+    if (n) {
+        if (best) HIP_TRY(hipMemcpyAsync(best, b->d_best, n * 4, hipMemcpyDeviceToHost, s));
+        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_ov, n * 4, hipMemcpyDeviceToHost, s));
+        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_score, n * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return DICE_OK;
+}
+
+int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32_t* tki, double* tks,
+                               void* stream) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    dice_ctx* c = b->ctx;
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    const size_t n = (size_t)b->n;
+    if (n && !b->d_mov) return fail(DICE_E_STATE, "dice_batch_matrix was not run");
+    if (n) {
+        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_mov, n * c->T * 4, hipMemcpyDeviceToHost, s));
+        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_mscore, n * c->T * 8, hipMemcpyDeviceToHost, s));
+        if (tki && b->k_used) HIP_TRY(hipMemcpyAsync(tki, b->d_tki, n * b->k_used * 4, hipMemcpyDeviceToHost, s));
+        if (tks && b->k_used) HIP_TRY(hipMemcpyAsync(tks, b->d_tks, n * b->k_used * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return DICE_OK;
+}
+
+int dice_batch_result_ptrs(dice_batch* b, void** best, void** ov, void** score) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    if (best) *best = b->d_best;
+    if (ov) *ov = b->d_ov;
+    if (score) *score = b->d_score;
+    return DICE_OK;
+}
+
+static int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out) {
+    if (ctx->scratch && ctx->scratch->capacity >= n) {
+        *out = ctx->scratch;
+        return DICE_OK;
+    }
+    if (ctx->scratch) {
+        dice_batch_destroy(ctx->scratch);
+        ctx->scratch = nullptr;
+    }
+    int rc = dice_batch_create(ctx, std::max<int64_t>(n, 64), &ctx->scratch);
+    *out = ctx->scratch;
+    return rc;
+}
+
+int dice_match(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
+    if (!ctx || !f) return fail(DICE_E_ARG, "NULL ctx/files");
+    if (f->n_files == 0) return DICE_OK;
+    dice_batch* b = nullptr;
+    int rc = scratch_for(ctx, f->n_files, &b);
+    if (rc) return rc;
+    if ((rc = dice_batch_upload(b, f, nullptr))) return rc;
+    if ((rc = dice_batch_match(b, thr, nullptr))) return rc;
+    return dice_batch_download_match(b, best, ov, score, nullptr);
+}
+
+int dice_similarity_matrix(dice_ctx* ctx, const dice_files* f, uint32_t* ov, double* score, int32_t k,
+                           int32_t* tki, double* tks) {
+    if (!ctx || !f) return fail(DICE_E_ARG, "NULL ctx/files");
+    if (k < 0 || k > DICE_TOPK_MAX) return fail(DICE_E_ARG, "k out of range");
+    if (k > 0 && (!tki || !tks)) return fail(DICE_E_ARG, "top-k outputs required when k > 0");
+    if (f->n_files == 0) return DICE_OK;
+    dice_batch* b = nullptr;
+    int rc = scratch_for(ctx, f->n_files, &b);
+    if (rc) return rc;
+    if ((rc = dice_batch_upload(b, f, nullptr))) return rc;
+    if ((rc = dice_batch_matrix(b, k, nullptr))) return rc;
+    return dice_batch_download_matrix(b, ov, score, k > 0 ? tki : nullptr, k > 0 ? tks : nullptr, nullptr);
+}
+
+}  // extern "C"
