@@ -126,6 +126,13 @@ int dice_batch_result_ptrs(dice_batch *batch, void **best, void **overlap, void 
 /* Bytes of the resident tile layout per file (the kernel's algorithmic input stream). */
 int64_t dice_batch_bytes_per_file(const dice_batch *batch);
 
+/* Build step (no device needed): generate + compile the corpus-specialized sparse program
+ * with hiprtc for gfx950 and store it in the code-object cache; writes the cache path. */
+int dice_precompile(const dice_templates *templates, char *path, int32_t path_cap);
+/* Generated HIP source of the sparse program (introspection/tests). Returns its length,
+ * writes at most cap-1 bytes + NUL when buf != NULL, or -1 on bad input. */
+int64_t dice_program_source(const dice_templates *templates, char *buf, int64_t cap);
+
 const char *dice_last_error(void);
 
 #ifdef __cplusplus

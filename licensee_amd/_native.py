@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = (
     'dice_similarity_matrix', 'dice_batch_create', 'dice_batch_destroy', 'dice_batch_upload',
     'dice_batch_match', 'dice_batch_matrix', 'dice_batch_download_match',
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
-    'dice_last_error',
+    'dice_last_error', 'dice_precompile', 'dice_program_source',
 )
 
 
@@ -73,6 +73,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_result_ptrs': (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         'dice_batch_bytes_per_file': (i64, [vp]),
         'dice_last_error': (ctypes.c_char_p, []),
+        'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
+        'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -21,9 +21,16 @@
 
 #include "../../include/licensee_dice.h"
 #include "dice_common.h"
-#include "dice_program.h"
+#include "dice_internal.h"
 
 using namespace dice;
+
+namespace dice {
+std::string& last_error() {
+    static thread_local std::string err;
+    return err;
+}
+}  // namespace dice
 
 // ---------------------------------------------------------------------------------------
 // Kernels
@@ -102,34 +109,40 @@ __global__ __launch_bounds__(256) void dice_dense_match(
     }
 }
 
-// Top-k insertion (best-first, later template first among exact ties) over registers.
+// Top-k over KM register slots, sorted best-first: rank-and-shift insertion with selects only
+// (p = slots strictly outranking the candidate; a later template goes before equal-scored
+// earlier ones, dice.rb:39). Slots past the caller's k hold lower-ranked valid entries.
+template <int KM>
 struct TopK {
-    int32_t idx[kTopKMax];
-    uint32_t ov[kTopKMax];
-    int32_t den[kTopKMax];
+    int32_t idx[KM];
+    uint32_t ov[KM];
+    int32_t den[KM];
     __device__ __forceinline__ void init() {
 #pragma unroll
-        for (int j = 0; j < kTopKMax; ++j) { idx[j] = -1; ov[j] = 0; den[j] = 1; }
+        for (int j = 0; j < KM; ++j) { idx[j] = -1; ov[j] = 0; den[j] = 1; }
     }
-    __device__ __forceinline__ void offer(int k, int32_t t, uint32_t o, int32_t d) {
-        bool carrying = true, placed = false;
-        int32_t ci = t; uint32_t co = o; int32_t cd = d;
+    __device__ __forceinline__ void offer(int32_t t, uint32_t o, int32_t d) {
+        int p = 0;
 #pragma unroll
-        for (int j = 0; j < kTopKMax; ++j) {
-            if (j < k && carrying) {
-                if (idx[j] < 0) {
-                    idx[j] = ci; ov[j] = co; den[j] = cd; carrying = false;
-                } else if (placed || dice_ge(co, cd, ov[j], den[j])) {
-                    const int32_t ti = idx[j]; const uint32_t to = ov[j]; const int32_t td = den[j];
-                    idx[j] = ci; ov[j] = co; den[j] = cd;
-                    ci = ti; co = to; cd = td; placed = true;
-                }
-            }
+        for (int j = 0; j < KM; ++j) p += (idx[j] >= 0 && !dice_ge(o, d, ov[j], den[j])) ? 1 : 0;
+#pragma unroll
+        for (int j = KM - 1; j > 0; --j) {
+            const bool mv = j > p;
+            idx[j] = mv ? idx[j - 1] : idx[j];
+            ov[j] = mv ? ov[j - 1] : ov[j];
+            den[j] = mv ? den[j - 1] : den[j];
+        }
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const bool put = j == p;
+            idx[j] = put ? t : idx[j];
+            ov[j] = put ? o : ov[j];
+            den[j] = put ? d : den[j];
         }
     }
 };
 
-template <int TT>
+template <int TT, int KM>
 __global__ __launch_bounds__(256) void dice_dense_matrix(
     const uint4* __restrict__ files, int64_t n, int32_t wq, const uint4* __restrict__ tq,
     const int4* __restrict__ tc, int32_t T, int32_t tpad, const uint32_t* __restrict__ wf,
@@ -146,7 +159,7 @@ __global__ __launch_bounds__(256) void dice_dense_matrix(
     const int32_t my_len = lenf[file];
     const bool my_cc = ccfp[file] != 0;
 
-    TopK top;
+    TopK<KM> top;
     top.init();
     for (int t0 = 0; t0 < T; t0 += TT) {
         uint32_t acc[TT];
@@ -169,13 +182,13 @@ __global__ __launch_bounds__(256) void dice_dense_matrix(
                     if (ov_out) ov_out[file * T + t] = acc[j];
                     if (score_out) score_out[file * T + t] = dice_score(acc[j], den);
                 }
-                if (!(c.w && my_cc)) top.offer(k, t, acc[j], den);
+                if (!(c.w && my_cc)) top.offer(t, acc[j], den);
             }
         }
     }
     if (valid && topk_idx) {
 #pragma unroll
-        for (int j = 0; j < kTopKMax; ++j) {
+        for (int j = 0; j < KM; ++j) {
             if (j < k) {
                 topk_idx[file * k + j] = top.idx[j];
                 topk_score[file * k + j] = top.idx[j] >= 0 ? dice_score(top.ov[j], top.den[j]) : -1.0;
@@ -188,13 +201,6 @@ __global__ __launch_bounds__(256) void dice_dense_matrix(
 // Host side
 // ---------------------------------------------------------------------------------------
 namespace {
-
-thread_local std::string g_err;
-
-int fail(int code, const std::string& msg) {
-    g_err = msg;
-    return code;
-}
 
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \
@@ -229,55 +235,13 @@ int dalloc(T** p, size_t count) {
 
 }  // namespace
 
-struct dice_ctx {
-    int device = 0;
-    int32_t T = 0, V = 0, w64 = 0, wq = 0, tpad = 0;
-    hipStream_t stream = nullptr;
-    uint4* d_tq = nullptr;  // [wq][tpad]
-    int4* d_tc = nullptr;   // [tpad]
-    int32_t kind = 0;       // 0 dense, 1 sparse program
-    dice::Program prog;     // sparse program (kind 1)
-    hipModule_t module = nullptr;
-    hipFunction_t prog_match = nullptr;
-    hipFunction_t prog_matrix = nullptr;
-    dice_batch* scratch = nullptr;  // reused by the host-buffer calls
-};
-
-struct dice_batch {
-    dice_ctx* ctx = nullptr;
-    int64_t capacity = 0, n = 0, n_tiles_cap = 0;
-    uint64_t* d_rows = nullptr;     // staging [capacity][w64]
-    uint4* d_tiles = nullptr;       // [n_tiles][wq][64]
-    uint32_t* d_wf = nullptr;
-    int32_t* d_len = nullptr;
-    uint8_t* d_cc = nullptr;
-    int32_t* d_best = nullptr;
-    uint32_t* d_ov = nullptr;
-    double* d_score = nullptr;
-    // matrix results (lazily allocated)
-    int64_t mat_cap = 0;
-    int32_t mat_k = 0;
-    int32_t k_used = 0;
-    uint32_t* d_mov = nullptr;
-    double* d_mscore = nullptr;
-    int32_t* d_tki = nullptr;
-    double* d_tks = nullptr;
-};
-
-namespace dice {
-// Stage 1: dense kernel for every corpus (the sparse program is selected in a later stage).
-int program_setup(dice_ctx* c, const dice_templates*) { c->kind = 0; return DICE_OK; }
-int program_launch_match(dice_ctx*, dice_batch*, double, hipStream_t) { return fail(DICE_E_STATE, "no program"); }
-int program_launch_matrix(dice_ctx*, dice_batch*, int32_t, hipStream_t) { return fail(DICE_E_STATE, "no program"); }
-}  // namespace dice
-
 static hipStream_t pick_stream(dice_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
 
 extern "C" {
 
 int32_t dice_words64(int32_t n_vocab) { return n_vocab <= 0 ? 0 : (n_vocab + 63) / 64; }
 
-const char* dice_last_error(void) { return g_err.c_str(); }
+const char* dice_last_error(void) { return dice::last_error().c_str(); }
 
 static void ctx_free(dice_ctx* c) {
     if (!c) return;
@@ -340,7 +304,7 @@ int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
         return fail(DICE_E_DEVICE, "template upload failed");
     }
     // Sparse-program kernel for small corpora (see dice_program.h).
-    rc = dice::program_setup(c, t);
+    rc = dice::program_setup(c, t);  // selects kind 1 when T <= kProgramMaxTemplates
     if (rc != DICE_OK) {
         ctx_free(c);
         return rc;
@@ -485,9 +449,14 @@ int dice_batch_matrix(dice_batch* b, int32_t k, void* stream) {
         rc = dice::program_launch_matrix(c, b, k, s);
         if (rc != DICE_OK) return rc;
     } else {
-        hipLaunchKernelGGL(dice_dense_matrix<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
-                           c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, k, b->d_mov,
-                           b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks);
+        if (k <= 4)
+            hipLaunchKernelGGL((dice_dense_matrix<kTT, 4>), dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n,
+                               c->wq, c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, k, b->d_mov,
+                               b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks);
+        else
+            hipLaunchKernelGGL((dice_dense_matrix<kTT, kTopKMax>), dim3(grid), dim3(kBlock), 0, s, b->d_tiles,
+                               b->n, c->wq, c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, k,
+                               b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks);
     }
     HIP_TRY(hipGetLastError());
     return DICE_OK;

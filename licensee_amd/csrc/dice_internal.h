@@ -1,0 +1,60 @@
+// Internal definitions shared by dice.hip and dice_program.cpp (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/licensee_dice.h"
+#include "dice_program.h"
+
+namespace dice {
+
+constexpr int32_t kProgramMaxTemplates = 64;   // sparse program kernel for T <= 64
+
+// thread-local last-error text (dice_last_error)
+std::string& last_error();
+
+inline int fail(int code, const std::string& msg) {
+    last_error() = msg;
+    return code;
+}
+
+}  // namespace dice
+
+struct dice_ctx {
+    int device = 0;
+    int32_t T = 0, V = 0, w64 = 0, wq = 0, tpad = 0;
+    hipStream_t stream = nullptr;
+    uint4* d_tq = nullptr;  // [wq][tpad] template quads (dense kernel)
+    int4* d_tc = nullptr;   // [tpad] TplConst (dense kernel)
+    int32_t kind = 0;       // 0 dense, 1 sparse program
+    dice::Program prog;     // sparse program (kind 1)
+    hipModule_t module = nullptr;
+    hipFunction_t prog_match = nullptr;
+    hipFunction_t prog_matrix = nullptr;    // top-k <= 4
+    hipFunction_t prog_matrix16 = nullptr;  // top-k <= 16
+    dice_batch* scratch = nullptr;  // reused by the host-buffer calls
+};
+
+struct dice_batch {
+    dice_ctx* ctx = nullptr;
+    int64_t capacity = 0, n = 0, n_tiles_cap = 0;
+    uint64_t* d_rows = nullptr;     // staging [capacity][w64]
+    uint4* d_tiles = nullptr;       // [n_tiles][wq][64]
+    uint32_t* d_wf = nullptr;
+    int32_t* d_len = nullptr;
+    uint8_t* d_cc = nullptr;
+    int32_t* d_best = nullptr;
+    uint32_t* d_ov = nullptr;
+    double* d_score = nullptr;
+    // matrix results (lazily allocated)
+    int64_t mat_cap = 0;
+    int32_t mat_k = 0;
+    int32_t k_used = 0;
+    uint32_t* d_mov = nullptr;
+    double* d_mscore = nullptr;
+    int32_t* d_tki = nullptr;
+    double* d_tks = nullptr;
+};

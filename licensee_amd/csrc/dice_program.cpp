@@ -1,0 +1,397 @@
+// Template-specialized sparse scoring program for small corpora (T <= 64), gfx950.
+//
+// The corpus is known when dice_create() runs, so the overlap loop
+//     ov_t = sum_d popcount(file[d] & Lf_t[d])          (content_helper.rb:129)
+// is emitted as straight-line HIP over the NONZERO (template, dword) pairs only: every file
+// dword lives in a VGPR with a compile-time index and every template mask is an instruction
+// literal, so an entry costs v_and_b32 (literal) + v_bcnt_u32_b32 (accumulate) and no
+// memory traffic beyond the file's own bitset. With the interner's signature vocabulary
+// order the 47 vendored templates need ~1.5k entries instead of 47 x 112 dense dwords,
+// which moves the kernel from VALU-bound to HBM-bound.
+//
+// Each template's epilogue follows its accumulation: denominator
+// (content_helper.rb:130-132,337-347, per-template constants baked in), CC filter
+// (dice.rb:23-31) and the running argmax (dice.rb:34-48). The compare is an exact
+// rational cross-multiplication on the fast path; waves holding a file outside the fast
+// envelope (|W_F| >= 2^20 or len_F >= 2^21, or a corpus outside the envelope) run the same
+// program with IEEE-double compares (see dice_common.h for why both orders coincide).
+//
+// The source is compiled with hiprtc for gfx950 and cached by hash under the library
+// directory (lib/cache/dice_prog_<hash>.co), so a corpus compiles once per machine image.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <sys/stat.h>
+#include <unistd.h>
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/licensee_dice.h"
+#include "dice_program.h"
+
+// dice_ctx / dice_batch internals shared with dice.hip
+#include "dice_internal.h"
+
+namespace dice {
+
+namespace {
+
+const char* kPrelude = R"HIP(
+typedef unsigned int u32;
+typedef int i32;
+typedef unsigned long long u64;
+typedef long long i64;
+
+__device__ __forceinline__ i32 dn(i32 base, i32 slack, i32 tlen, u32 wf, i32 lf) {
+    i32 d = tlen - lf;
+    d = d < 0 ? -d : d;
+    i32 adj = slack < 0 ? d : (d - slack > 0 ? d - slack : 0);
+    return base + (i32)wf + adj / 4;
+}
+__device__ __forceinline__ double sc(u32 o, i32 d) { return ((double)o * 200.0) / (double)d; }
+template <bool FAST>
+__device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
+    if (FAST) return (u64)oa * (u64)(u32)db >= (u64)ob * (u64)(u32)da;
+    return sc(oa, da) >= sc(ob, db);
+}
+#define ACC(d, m) a = __builtin_popcount(f[d] & (m##u)) + a
+#define ACCF(d) a = __builtin_popcount(f[d]) + a
+)HIP";
+
+const char* kMatchKernel = R"HIP(
+extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
+    const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
+    const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
+    u32* __restrict__ ov_out, double* __restrict__ score_out) {
+    const int lane = threadIdx.x & 63;
+    const i64 tile = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile * 64 >= n) return;
+    const i64 file = tile * 64 + lane;
+    const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
+    u32 f[WQ * 4];
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+        const uint4 v = fp[q * 64];
+        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+    }
+    const u32 wf = wfp[file];
+    const i32 lf = lenp[file];
+    const bool cc = ccp[file] != 0;
+    const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
+    i32 bi = -1; u32 bo = 0; i32 bd = 1;
+    if (__all(fast)) {
+        PROGRAM(true)
+    } else {
+        PROGRAM(false)
+    }
+    if (file < n) {
+        const double s = bi >= 0 ? sc(bo, bd) : 0.0;
+        best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
+        ov_out[file] = bo;
+        score_out[file] = s;
+    }
+}
+)HIP";
+
+// Matrix kernel template: KM is the compile-time top-k slot count (4 or 16).
+const char* kMatrixKernel = R"HIP(
+extern "C" __global__ __launch_bounds__(256) void KNAME(
+    const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
+    const unsigned char* __restrict__ ccp, i32 k, u32* __restrict__ ov_out, double* __restrict__ score_out,
+    i32* __restrict__ topk_idx, double* __restrict__ topk_score) {
+    const int lane = threadIdx.x & 63;
+    const i64 tile = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile * 64 >= n) return;
+    const i64 file = tile * 64 + lane;
+    const bool valid = file < n;
+    const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
+    u32 f[WQ * 4];
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+        const uint4 v = fp[q * 64];
+        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+    }
+    const u32 wf = wfp[file];
+    const i32 lf = lenp[file];
+    const bool cc = ccp[file] != 0;
+    const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
+    i32 ti[KM]; u32 to[KM]; i32 td[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) { ti[j] = -1; to[j] = 0; td[j] = 1; }
+    u32* orow = ov_out ? ov_out + file * NT : nullptr;
+    double* srow = score_out ? score_out + file * NT : nullptr;
+    if (__all(fast)) {
+        MATRIX_PROGRAM(true)
+    } else {
+        MATRIX_PROGRAM(false)
+    }
+    if (valid && topk_idx) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j < k) {
+                topk_idx[file * k + j] = ti[j];
+                topk_score[file * k + j] = ti[j] >= 0 ? sc(to[j], td[j]) : -1.0;
+            }
+        }
+    }
+}
+)HIP";
+
+// Per-template matrix epilogue: store the row entry, then rank-and-shift insertion into the
+// KM sorted slots (p = slots that strictly outrank the candidate; a later template goes
+// before equal-scored earlier ones, dice.rb:39). Branch-free selects only.
+const char* kMatrixOffer = R"HIP(
+#define MOFFER(T, CCF)                                                                  \
+    {                                                                                   \
+        if (valid) { if (orow) orow[T] = a; if (srow) srow[T] = sc(a, d); }            \
+        if (!((CCF) && cc)) {                                                           \
+            int p = 0;                                                                  \
+            _Pragma("unroll") for (int j = 0; j < KM; ++j)                              \
+                p += (ti[j] >= 0 && !ge<FASTV>(a, d, to[j], td[j])) ? 1 : 0;           \
+            _Pragma("unroll") for (int j = KM - 1; j > 0; --j) {                        \
+                const bool mv = j > p;                                                  \
+                ti[j] = mv ? ti[j - 1] : ti[j];                                         \
+                to[j] = mv ? to[j - 1] : to[j];                                         \
+                td[j] = mv ? td[j - 1] : td[j];                                         \
+            }                                                                           \
+            _Pragma("unroll") for (int j = 0; j < KM; ++j) {                            \
+                const bool put = j == p;                                                \
+                ti[j] = put ? (T) : ti[j];                                              \
+                to[j] = put ? a : to[j];                                                \
+                td[j] = put ? d : td[j];                                                \
+            }                                                                           \
+        }                                                                               \
+    }
+)HIP";
+
+uint64_t fnv1a(const std::string& s) {
+    uint64_t h = 1469598103934665603ULL;
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 1099511628211ULL;
+    }
+    return h;
+}
+
+std::string lib_dir() {
+    Dl_info info;
+    if (dladdr((void*)&fnv1a, &info) && info.dli_fname) {
+        std::string p(info.dli_fname);
+        size_t s = p.rfind('/');
+        if (s != std::string::npos) return p.substr(0, s);
+    }
+    return ".";
+}
+
+std::string cache_dir() {
+    const char* env = getenv("DICE_CACHE_DIR");
+    std::string d = env && *env ? std::string(env) : lib_dir() + "/cache";
+    mkdir(d.c_str(), 0755);
+    return d;
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return false;
+    out.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+    return !out.empty();
+}
+
+}  // namespace
+
+// Build the entry list (template-major, dword ascending) from the template bitsets.
+static void build_entries(const dice_templates* t, int32_t w64, Program& p) {
+    p.prog.clear();
+    const int32_t w32 = w64 * 2;
+    for (int32_t i = 0; i < t->n_templates; ++i) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(t->lf_bits + (size_t)i * w64);
+        for (int32_t d = 0; d < w32; ++d)
+            if (row[d]) p.prog.push_back(Entry{i, d, row[d]});
+    }
+}
+
+std::string program_source(const dice_templates* t, const Program& p, int32_t wq, bool corpus_fast) {
+    std::ostringstream s;
+    const char* waves = getenv("DICE_PROG_WAVES");  // optional occupancy floor (waves/SIMD) for A/B runs
+    s << "#define MATCH_WAVES " << (waves && *waves ? std::string(", ") + waves : std::string()) << "\n";
+    s << "#define WQ " << wq << "\n#define NT " << t->n_templates << "\n#define CORPUS_FAST "
+      << (corpus_fast ? 1 : 0) << "\n" << kPrelude;
+    // match program
+    std::ostringstream body, mbody;
+    size_t e = 0;
+    for (int32_t i = 0; i < t->n_templates; ++i) {
+        std::ostringstream acc;
+        acc << "a = 0; ";
+        for (; e < p.prog.size() && p.prog[e].tpl == i; ++e) {
+            const Entry& en = p.prog[e];
+            if (en.mask == 0xFFFFFFFFu) acc << "ACCF(" << en.dword << "); ";
+            else acc << "ACC(" << en.dword << ", 0x" << std::hex << en.mask << std::dec << "); ";
+        }
+        const int32_t base = (int32_t)t->lf_size[i] - (int32_t)t->fields_set_size[i];
+        std::ostringstream den;
+        den << "d = dn(" << base << ", " << t->length_slack[i] << ", " << t->length[i] << ", wf, lf); ";
+        const int cc = t->is_cc[i] ? 1 : 0;
+        body << "{ u32 a; i32 d; " << acc.str() << den.str();
+        if (cc) body << "if (!cc) ";
+        body << "{ if ((!FASTV && bi < 0) || ge<FASTV>(a, d, bo, bd)) { bi = " << i
+             << "; bo = a; bd = d; } } }\n";
+        mbody << "{ u32 a; i32 d; " << acc.str() << den.str() << "MOFFER(" << i << ", " << cc << ") }\n";
+    }
+    s << "#define PROGRAM(FASTV_) { constexpr bool FASTV = FASTV_; \\\n";
+    std::string b = body.str();
+    // one macro line per statement
+    std::istringstream lines(b);
+    std::string line;
+    while (std::getline(lines, line)) s << line << " \\\n";
+    s << "}\n";
+    s << kMatchKernel;
+    s << kMatrixOffer;
+    s << "#define MATRIX_PROGRAM(FASTV_) { constexpr bool FASTV = FASTV_; \\\n";
+    std::istringstream ml(mbody.str());
+    while (std::getline(ml, line)) s << line << " \\\n";
+    s << "}\n";
+    for (int km : {4, 16}) {
+        s << "#define KM " << km << "\n#define KNAME dice_prog_matrix" << km << "\n" << kMatrixKernel
+          << "#undef KM\n#undef KNAME\n";
+    }
+    return s.str();
+}
+
+// Compile (or find in the cache) the code object for `src`. No device needed.
+static int compile_cached(const std::string& src, std::vector<char>& code, std::string* path_out) {
+    const uint64_t h = fnv1a(src);
+    char name[64];
+    snprintf(name, sizeof(name), "dice_prog_%016llx.co", (unsigned long long)h);
+    const std::string path = cache_dir() + "/" + name;
+    if (!read_file(path, code)) {
+        hiprtcProgram prog;
+        if (hiprtcCreateProgram(&prog, src.c_str(), "dice_prog.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+            return fail(DICE_E_DEVICE, "hiprtcCreateProgram failed");
+        const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+        hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+        if (r != HIPRTC_SUCCESS) {
+            size_t ls = 0;
+            hiprtcGetProgramLogSize(prog, &ls);
+            std::string log(ls, '\0');
+            if (ls) hiprtcGetProgramLog(prog, &log[0]);
+            hiprtcDestroyProgram(&prog);
+            return fail(DICE_E_DEVICE, "hiprtc compile failed: " + log.substr(0, 2000));
+        }
+        size_t cs = 0;
+        hiprtcGetCodeSize(prog, &cs);
+        code.resize(cs);
+        hiprtcGetCode(prog, code.data());
+        hiprtcDestroyProgram(&prog);
+        // best-effort cache write (atomic rename)
+        const std::string tmp = path + ".tmp." + std::to_string(getpid());
+        {
+            std::ofstream out(tmp, std::ios::binary);
+            if (out) out.write(code.data(), (std::streamsize)code.size());
+        }
+        rename(tmp.c_str(), path.c_str());
+    }
+    if (path_out) *path_out = path;
+    return DICE_OK;
+}
+
+static int compile_or_load(dice_ctx* c, const std::string& src) {
+    std::vector<char> code;
+    int rc = compile_cached(src, code, nullptr);
+    if (rc != DICE_OK) return rc;
+    if (hipModuleLoadData(&c->module, code.data()) != hipSuccess) return fail(DICE_E_DEVICE, "hipModuleLoadData failed");
+    if (hipModuleGetFunction(&c->prog_match, c->module, "dice_prog_match") != hipSuccess ||
+        hipModuleGetFunction(&c->prog_matrix, c->module, "dice_prog_matrix4") != hipSuccess ||
+        hipModuleGetFunction(&c->prog_matrix16, c->module, "dice_prog_matrix16") != hipSuccess)
+        return fail(DICE_E_DEVICE, "hipModuleGetFunction failed");
+    return DICE_OK;
+}
+
+static bool corpus_in_fast_envelope(const dice_templates* t) {
+    // static fast-path envelope (dice_common.h): base >= 1, base < 2^18, len < 2^20,
+    // 200*|Lf| < 1024*base  =>  every fast-file denominator is in [1, 2^21), scores < 1024.
+    for (int32_t i = 0; i < t->n_templates; ++i) {
+        const int64_t base = (int64_t)t->lf_size[i] - (int64_t)t->fields_set_size[i];
+        if (!(base >= 1 && base < (1 << 18) && t->length[i] >= 0 && t->length[i] < (1 << 20) &&
+              200 * (int64_t)t->lf_size[i] < 1024 * base))
+            return false;
+    }
+    return true;
+}
+
+static std::string source_for(const dice_templates* t, Program& prog) {
+    const int32_t w64 = (t->n_vocab + 63) / 64;
+    build_entries(t, w64, prog);
+    return program_source(t, prog, (w64 + 1) / 2, corpus_in_fast_envelope(t));
+}
+
+bool program_wanted(const dice_templates* t) {
+    const char* force = getenv("DICE_FORCE_DENSE");
+    return !(force && *force == '1') && t->n_templates <= kProgramMaxTemplates;
+}
+
+int program_setup(dice_ctx* c, const dice_templates* t) {
+    c->kind = 0;
+    if (!program_wanted(t)) return DICE_OK;
+    const std::string src = source_for(t, c->prog);
+    int rc = compile_or_load(c, src);
+    if (rc != DICE_OK) return rc;
+    c->kind = 1;
+    return DICE_OK;
+}
+
+int program_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    const int64_t n_tiles = (b->n + 63) / 64;
+    const unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    int64_t n = b->n;
+    void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score};
+    if (hipModuleLaunchKernel(c->prog_match, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+        return fail(DICE_E_DEVICE, "launch dice_prog_match failed");
+    return DICE_OK;
+}
+
+int program_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s) {
+    const int64_t n_tiles = (b->n + 63) / 64;
+    const unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    int64_t n = b->n;
+    int32_t kk = k;
+    int32_t* tki = k > 0 ? b->d_tki : nullptr;
+    double* tks = k > 0 ? b->d_tks : nullptr;
+    void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &kk, &b->d_mov, &b->d_mscore, &tki, &tks};
+    hipFunction_t fn = k <= 4 ? c->prog_matrix : c->prog_matrix16;
+    if (hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+        return fail(DICE_E_DEVICE, "launch dice_prog_matrix failed");
+    return DICE_OK;
+}
+
+}  // namespace dice
+
+extern "C" int dice_precompile(const dice_templates* t, char* path, int32_t path_cap) {
+    if (!t || t->n_templates < 1 || t->n_vocab < 1 || !t->lf_bits) return dice::fail(DICE_E_ARG, "invalid dice_templates");
+    if (!dice::program_wanted(t)) return dice::fail(DICE_E_STATE, "corpus uses the dense kernel");
+    dice::Program prog;
+    const std::string src = dice::source_for(t, prog);
+    std::vector<char> code;
+    std::string p;
+    int rc = dice::compile_cached(src, code, &p);
+    if (rc == DICE_OK && path && path_cap > 0) snprintf(path, (size_t)path_cap, "%s", p.c_str());
+    return rc;
+}
+
+extern "C" int64_t dice_program_source(const dice_templates* t, char* buf, int64_t cap) {
+    if (!t || t->n_templates < 1 || t->n_vocab < 1 || !t->lf_bits) return -1;
+    dice::Program prog;
+    const std::string src = dice::source_for(t, prog);
+    if (buf && cap > 0) {
+        const size_t n = std::min<size_t>((size_t)cap - 1, src.size());
+        memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return (int64_t)src.size();
+}

@@ -82,3 +82,17 @@ def pair_similarity(a, b) -> float:
         return row[0]
     finally:
         eng.scorer.close()
+
+
+def precompile_default() -> str:
+    """Build step: compile + cache the sparse program for the vendored corpus (no device)."""
+    import ctypes
+
+    from . import _native
+    lib = _native.load_library()
+    c = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    keep = [c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc]
+    t = _native._Templates(len(c.lf_size), c.n_vocab, *[k.ctypes.data for k in keep])
+    path = ctypes.create_string_buffer(1024)
+    _native._check(lib.dice_precompile(ctypes.byref(t), path, 1024))
+    return path.value.decode()

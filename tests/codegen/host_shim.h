@@ -1,0 +1,13 @@
+// Host shim to compile the generated sparse-program kernels (dice_program.cpp) with g++
+// for CPU tests: one "lane" per call, wave votes degenerate to the lane's own value.
+#pragma once
+#include <stdint.h>
+#define __global__
+#define __device__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __restrict__ __restrict
+struct uint4 { unsigned x, y, z, w; };
+struct Dim3 { unsigned x; };
+static Dim3 threadIdx, blockIdx;
+static inline bool __all(bool v) { return v; }

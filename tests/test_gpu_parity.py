@@ -18,10 +18,24 @@ def templates():
     return License.all(hidden=True, pseudo=False)
 
 
-@pytest.fixture(scope='module')
-def engine(templates):
+@pytest.fixture(scope='module', params=['program', 'dense'])
+def engine(request, templates, monkeypatch_module):
     from licensee_amd.dice import DiceEngine
-    return DiceEngine(templates, device=0)
+    if request.param == 'dense':
+        monkeypatch_module.setenv('DICE_FORCE_DENSE', '1')
+    else:
+        monkeypatch_module.delenv('DICE_FORCE_DENSE', raising=False)
+    eng = DiceEngine(templates, device=0)
+    assert eng.scorer.info()[2] == (1 if request.param == 'program' else 0)
+    yield eng
+    eng.scorer.close()
+
+
+@pytest.fixture(scope='module')
+def monkeypatch_module():
+    mp = pytest.MonkeyPatch()
+    yield mp
+    mp.undo()
 
 
 @pytest.fixture(scope='module')

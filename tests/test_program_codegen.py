@@ -1,0 +1,97 @@
+"""CPU test of the generated sparse-program kernels (csrc/dice_program.cpp).
+
+The HIP source the library generates for a corpus is compiled for the HOST with g++ under a
+small shim (tests/codegen/host_shim.h) and run lane by lane; results must equal the C
+oracle bit-for-bit. This checks the code generator (entry list, baked-in constants, CC
+masks, argmax / top-k epilogues, fast/slow compare paths) without a GPU.
+"""
+import ctypes
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.helpers import NormFile, make_files
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def tile_pack(bits: np.ndarray, wq: int) -> np.ndarray:
+    """Row-major [n][w64] uint64 -> tile layout [n_tiles][wq][64] of 4 x uint32."""
+    n, w64 = bits.shape
+    nt = (n + 63) // 64
+    d32 = np.zeros((nt * 64, wq * 4), np.uint32)
+    d32[:n, :w64 * 2] = bits.view(np.uint32).reshape(n, w64 * 2)
+    return np.ascontiguousarray(d32.reshape(nt, 64, wq, 4).transpose(0, 2, 1, 3))
+
+
+def _templates_struct(corpus):
+    from licensee_amd import _native
+    keep = [np.ascontiguousarray(x) for x in (corpus.lf_bits, corpus.lf_size, corpus.fields_set_size,
+                                              corpus.length_slack, corpus.length, corpus.is_cc)]
+    return keep, _native._Templates(len(corpus.lf_size), corpus.n_vocab, *[k.ctypes.data for k in keep])
+
+
+def generated_source(corpus) -> str:
+    from licensee_amd import _native
+    lib = _native.load_library()
+    keep, t = _templates_struct(corpus)
+    n = lib.dice_program_source(ctypes.byref(t), None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.dice_program_source(ctypes.byref(t), buf, n + 1)
+    return buf.value.decode()
+
+
+def run_host(corpus, fb, k, tmp_path):
+    src = generated_source(corpus)
+    d = str(tmp_path)
+    with open(os.path.join(d, 'prog.inc'), 'w') as fh:
+        fh.write(src)
+    shutil.copy(os.path.join(HERE, 'codegen', 'host_shim.h'), d)
+    exe = os.path.join(d, 'drv')
+    subprocess.run(['g++', '-O1', '-std=c++17', '-w', '-I', d, '-o', exe, os.path.join(HERE, 'codegen', 'driver.cpp')],
+                   check=True)
+    wq = (corpus.w64 + 1) // 2
+    n = fb.n
+    npad = ((n + 63) // 64) * 64
+    tile_pack(fb.bits, wq).tofile(os.path.join(d, 'tiles.bin'))
+    for name, arr, dt in (('wf', fb.wordset_size, np.uint32), ('len', fb.length, np.int32),
+                          ('cc', fb.cc_false_positive, np.uint8)):
+        pad = np.zeros(npad, dt)
+        pad[:n] = arr
+        pad.tofile(os.path.join(d, name + '.bin'))
+    subprocess.run([exe, d, str(n), str(k)], check=True)
+    T = corpus.lf_bits.shape[0]
+    rd = lambda name, dt: np.fromfile(os.path.join(d, name), dt)
+    return (rd('best.out', np.int32), rd('ov.out', np.uint32), rd('score.out', np.float64),
+            rd('mov.out', np.uint32).reshape(n, T), rd('msc.out', np.float64).reshape(n, T),
+            rd('tki.out', np.int32).reshape(n, max(k, 1))[:, :k], rd('tks.out', np.float64).reshape(n, max(k, 1))[:, :k])
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+@pytest.mark.parametrize('k', [3, 5])
+def test_generated_program_matches_oracle(tmp_path, k):
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from oracle import dice_oracle as O
+    from oracle.native import OracleScorer
+    from tests.helpers import oracle_templates
+
+    templates = License.all(hidden=True, pseudo=False)
+    corpus = TemplateCorpus(templates)
+    files = make_files(templates, 150, 21) + [NormFile(''), NormFile('x' * 10, cc=True)]
+    fb = corpus.intern_files(files)
+    best, ov, score, mov, msc, tki, tks = run_host(corpus, fb, k, tmp_path)
+    orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                       corpus.length, corpus.is_cc, corpus.n_vocab)
+    eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0)
+    assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+    emov, emsc = orc.matrix(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive)
+    assert np.array_equal(mov, emov) and np.array_equal(msc, emsc)
+    otpl = oracle_templates(templates)
+    for i, f in enumerate(files):
+        ranked = O.matches_by_similarity(otpl, f.oracle, cc_fp=f.cc)[:k]
+        assert tki[i].tolist() == [r[0] for r in ranked] + [-1] * (k - len(ranked)), i
+        assert tks[i, :len(ranked)].tolist() == [r[1] for r in ranked], i
