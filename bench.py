@@ -64,6 +64,7 @@ def main():
     ap.add_argument('--topk', type=int, default=3)
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU-work budget of the baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--probe', action='store_true', help='diagnostic: stream-read the tiles only (read ceiling)')
     args = ap.parse_args()
 
     import torch
@@ -104,7 +105,9 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        if cfg == 5:
+        if args.probe:
+            batch.stream_probe(sptr)
+        elif cfg == 5:
             batch.matrix(args.topk, sptr)
         else:
             batch.match(args.threshold, sptr)
@@ -144,6 +147,7 @@ def main():
     algo_bytes_per_file = tile_bytes + 4 + 4 + 1 + out_bytes
     achieved = algo_bytes_per_file * n_per / (launch_ms * 1e-3) / 1e9
     traffic = None
+    traffic_src = None
     pmc_path = os.path.join(ROOT, 'profiles', f'pmc_config{cfg}.json')
     if os.path.exists(pmc_path):
         try:
@@ -151,6 +155,7 @@ def main():
                 pmc = json.load(fh)
             if pmc.get('files_per_launch') == n_per and pmc.get('templates') == T:
                 traffic = pmc.get('hbm_bytes_per_launch')
+                traffic_src = f"profiles/pmc_config{cfg}.json ({pmc.get('tag')})"
         except Exception:
             traffic = None
 
@@ -244,6 +249,7 @@ def main():
                        'program_entries': entries, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'traffic_source': traffic_src,
                          'algorithmic_bytes_per_file': algo_bytes_per_file, 'launch_ms': launch_ms},
             'cpu_baseline': cpu_baseline,
             'scores_per_s': value * T,

@@ -123,6 +123,8 @@ int dice_batch_download_matrix(dice_batch *batch, uint32_t *overlap, double *sco
                                int32_t *topk_index, double *topk_score, void *stream);
 /* Device pointers of the match results (int32 best, uint32 overlap, double score). */
 int dice_batch_result_ptrs(dice_batch *batch, void **best, void **overlap, void **score);
+/* Diagnostic: stream-read the resident tiles with trivial compute (read-ceiling probe). */
+int dice_batch_stream_probe(dice_batch *batch, void *stream);
 /* Bytes of the resident tile layout per file (the kernel's algorithmic input stream). */
 int64_t dice_batch_bytes_per_file(const dice_batch *batch);
 

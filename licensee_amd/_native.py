@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = (
     'dice_similarity_matrix', 'dice_batch_create', 'dice_batch_destroy', 'dice_batch_upload',
     'dice_batch_match', 'dice_batch_matrix', 'dice_batch_download_match',
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
-    'dice_last_error', 'dice_precompile', 'dice_program_source',
+    'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
 )
 
 
@@ -72,6 +72,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_download_matrix': (ctypes.c_int, [vp, vp, vp, vp, vp, vp]),
         'dice_batch_result_ptrs': (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         'dice_batch_bytes_per_file': (i64, [vp]),
+        'dice_batch_stream_probe': (ctypes.c_int, [vp, vp]),
         'dice_last_error': (ctypes.c_char_p, []),
         'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
         'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
@@ -243,6 +244,9 @@ class DeviceBatch:
         p = [ctypes.c_void_p() for _ in range(3)]
         _check(load_library().dice_batch_result_ptrs(self._b, *[ctypes.byref(x) for x in p]))
         return tuple(x.value for x in p)
+
+    def stream_probe(self, stream: int = 0):
+        _check(load_library().dice_batch_stream_probe(self._b, stream or None))
 
     def bytes_per_file(self) -> int:
         return int(load_library().dice_batch_bytes_per_file(self._b))

@@ -57,6 +57,25 @@ __global__ __launch_bounds__(256) void dice_pack_tiles(const uint64_t* __restric
     tiles[gid] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 
+// Diagnostic: pure streaming read of the resident tile layout (same addresses and widths as
+// the scorers, trivial compute, 16 B written per file). Measures the read ceiling that the
+// Dice kernels are judged against (DESIGN.md "roofline").
+__global__ __launch_bounds__(256) void dice_stream_probe(const uint4* __restrict__ files, int64_t n, int32_t wq,
+                                                         uint4* __restrict__ out) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    if (tile * kWave >= n) return;
+    const uint4* fp = files + tile * (int64_t)wq * kWave + lane;
+    uint4 x = make_uint4(0, 0, 0, 0);
+#pragma unroll 8
+    for (int q = 0; q < wq; ++q) {
+        const uint4 v = fp[(int64_t)q * kWave];
+        x.x ^= v.x; x.y ^= v.y; x.z ^= v.z; x.w ^= v.w;
+    }
+    const int64_t file = tile * kWave + lane;
+    if (file < n) out[file] = x;
+}
+
 __device__ __forceinline__ uint32_t popc_and4(uint4 f, uint4 m) {
     return __popc(f.x & m.x) + __popc(f.y & m.y) + __popc(f.z & m.z) + __popc(f.w & m.w);
 }
@@ -492,6 +511,22 @@ int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32
         if (tks && b->k_used) HIP_TRY(hipMemcpyAsync(tks, b->d_tks, n * b->k_used * 8, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
+    return DICE_OK;
+}
+
+int dice_batch_stream_probe(dice_batch* b, void* stream) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    dice_ctx* c = b->ctx;
+    if (b->n == 0) return DICE_OK;
+    if (c->w64 < 2) return fail(DICE_E_STATE, "probe needs >= 2 words per file");
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    const int64_t n_tiles = (b->n + kWave - 1) / kWave;
+    const unsigned grid = (unsigned)((n_tiles + (kBlock / kWave) - 1) / (kBlock / kWave));
+    // results land in the (16 B/file) score+best+overlap area: reuse d_score as scratch
+    hipLaunchKernelGGL(dice_stream_probe, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
+                       reinterpret_cast<uint4*>(b->d_rows));
+    HIP_TRY(hipGetLastError());
     return DICE_OK;
 }
 

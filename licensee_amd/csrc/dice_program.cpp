@@ -49,16 +49,31 @@ typedef int i32;
 typedef unsigned long long u64;
 typedef long long i64;
 
+#ifdef __HIP_DEVICE_COMPILE__
+// v_mul_u32_u24: full-rate 24x24 multiply (low 32 bits); v_sad_u32: |a - b| + c in one op.
+__device__ __forceinline__ u32 mul24(u32 a, u32 b) { u32 r; asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+__device__ __forceinline__ u32 absdiff(u32 a, u32 b) { u32 r; asm("v_sad_u32 %0, %1, %2, 0" : "=v"(r) : "s"(a), "v"(b)); return r; }
+#else
+__device__ __forceinline__ u32 mul24(u32 a, u32 b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+__device__ __forceinline__ u32 absdiff(u32 a, u32 b) { return a > b ? a - b : b - a; }
+#endif
+// Denominator (content_helper.rb:130-132,337-347); lengths are non-negative (len_F < 2^31).
 __device__ __forceinline__ i32 dn(i32 base, i32 slack, i32 tlen, u32 wf, i32 lf) {
-    i32 d = tlen - lf;
-    d = d < 0 ? -d : d;
+    const i32 d = (i32)absdiff((u32)tlen, (u32)lf);
     i32 adj = slack < 0 ? d : (d - slack > 0 ? d - slack : 0);
     return base + (i32)wf + adj / 4;
 }
 __device__ __forceinline__ double sc(u32 o, i32 d) { return ((double)o * 200.0) / (double)d; }
 template <bool FAST>
 __device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
-    if (FAST) return (u64)oa * (u64)(u32)db >= (u64)ob * (u64)(u32)da;
+    if (FAST) {
+#if NARROW_MUL
+        // ov < 2^11 and den < 2^21: both products < 2^32, full-rate 24-bit multiplies are exact
+        return mul24(oa, (u32)db) >= mul24(ob, (u32)da);
+#else
+        return (u64)oa * (u64)(u32)db >= (u64)ob * (u64)(u32)da;
+#endif
+    }
     return sc(oa, da) >= sc(ob, db);
 }
 #define ACC(d, m) a = __builtin_popcount(f[d] & (m##u)) + a
@@ -75,27 +90,65 @@ extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
     if (tile * 64 >= n) return;
     const i64 file = tile * 64 + lane;
     const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
-    u32 f[WQ * 4];
-#pragma unroll
-    for (int q = 0; q < WQ; ++q) {
-        const uint4 v = fp[q * 64];
-        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
-    }
     const u32 wf = wfp[file];
     const i32 lf = lenp[file];
     const bool cc = ccp[file] != 0;
+    FILE_PROLOGUE
     const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
     i32 bi = -1; u32 bo = 0; i32 bd = 1;
     if (__all(fast)) {
-        PROGRAM(true)
+        MATCH_BODY(true)
     } else {
-        PROGRAM(false)
+        MATCH_BODY(false)
     }
     if (file < n) {
         const double s = bi >= 0 ? sc(bo, bd) : 0.0;
         best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
         ov_out[file] = bo;
         score_out[file] = s;
+    }
+}
+)HIP";
+
+// Persistent match kernel: grid = resident capacity; each wave walks tiles tile, tile+stride...
+// and its quad prefetch ring keeps streaming across tile boundaries (PERSIST_BODY).
+const char* kMatchPersistKernel = R"HIP(
+extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match_p(
+    const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
+    const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
+    u32* __restrict__ ov_out, double* __restrict__ score_out) {
+    const int lane = threadIdx.x & 63;
+    const i64 ntiles = (n + 63) / 64;
+    const i64 stride = (i64)gridDim.x * 4;
+    i64 tile = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
+    PERSIST_PROLOGUE
+    for (;;) {
+        const i64 file = tile * 64 + lane;
+        const i64 next = tile + stride;
+        const bool has_next = next < ntiles;
+        const uint4* np = files + next * (i64)(WQ * 64) + lane;
+        const u32 wf = wfp[file];
+        const i32 lf = lenp[file];
+        const bool cc = ccp[file] != 0;
+        const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
+        PERSIST_STREAM
+        i32 bi = -1; u32 bo = 0; i32 bd = 1;
+        if (__all(fast)) {
+            MATCH_BODY(true)
+        } else {
+            MATCH_BODY(false)
+        }
+        if (file < n) {
+            const double s = bi >= 0 ? sc(bo, bd) : 0.0;
+            best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
+            ov_out[file] = bo;
+            score_out[file] = s;
+        }
+        if (!has_next) break;
+        tile = next;
+        fp = np;
     }
 }
 )HIP";
@@ -112,15 +165,10 @@ extern "C" __global__ __launch_bounds__(256) void KNAME(
     const i64 file = tile * 64 + lane;
     const bool valid = file < n;
     const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
-    u32 f[WQ * 4];
-#pragma unroll
-    for (int q = 0; q < WQ; ++q) {
-        const uint4 v = fp[q * 64];
-        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
-    }
     const u32 wf = wfp[file];
     const i32 lf = lenp[file];
     const bool cc = ccp[file] != 0;
+    FILE_PROLOGUE
     const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
     i32 ti[KM]; u32 to[KM]; i32 td[KM];
 #pragma unroll
@@ -128,9 +176,9 @@ extern "C" __global__ __launch_bounds__(256) void KNAME(
     u32* orow = ov_out ? ov_out + file * NT : nullptr;
     double* srow = score_out ? score_out + file * NT : nullptr;
     if (__all(fast)) {
-        MATRIX_PROGRAM(true)
+        MATRIX_BODY(true)
     } else {
-        MATRIX_PROGRAM(false)
+        MATRIX_BODY(false)
     }
     if (valid && topk_idx) {
 #pragma unroll
@@ -217,46 +265,140 @@ static void build_entries(const dice_templates* t, int32_t w64, Program& p) {
     }
 }
 
+// Emits `text` as the body of a one-line-per-statement macro.
+static void emit_macro(std::ostringstream& s, const std::string& head, const std::string& text) {
+    s << "#define " << head << " \\\n";
+    std::istringstream lines(text);
+    std::string line;
+    while (std::getline(lines, line)) s << line << " \\\n";
+    s << "\n";
+}
+
+// Program order:
+//   'd' (default) dword-major: every template accumulator stays live (acc[NT]); file quads are
+//       loaded one at a time right where they are consumed, so a file dword's live range is a
+//       few instructions and the kernel runs at far lower VGPR count / higher occupancy; the
+//       epilogue (denominator, compare) runs once per template after the last quad.
+//   't' template-major: the whole file bitset is loaded up front (WQ*4 VGPRs) and each
+//       template is accumulated and retired in turn.
 std::string program_source(const dice_templates* t, const Program& p, int32_t wq, bool corpus_fast) {
     std::ostringstream s;
     const char* waves = getenv("DICE_PROG_WAVES");  // optional occupancy floor (waves/SIMD) for A/B runs
+    const char* order_env = getenv("DICE_PROG_ORDER");
+    const char order = (order_env && *order_env == 't') ? 't' : 'd';
+    s << "// dice sparse program: T=" << t->n_templates << " V=" << t->n_vocab << " entries=" << p.prog.size()
+      << " order=" << order << "\n";
     s << "#define MATCH_WAVES " << (waves && *waves ? std::string(", ") + waves : std::string()) << "\n";
+    uint32_t max_lf = 0;
+    for (int32_t i = 0; i < t->n_templates; ++i) max_lf = std::max(max_lf, t->lf_size[i]);
     s << "#define WQ " << wq << "\n#define NT " << t->n_templates << "\n#define CORPUS_FAST "
-      << (corpus_fast ? 1 : 0) << "\n" << kPrelude;
-    // match program
-    std::ostringstream body, mbody;
-    size_t e = 0;
+      << (corpus_fast ? 1 : 0) << "\n#define NARROW_MUL " << (max_lf < (1u << 11) ? 1 : 0) << "\n" << kPrelude;
+
+    std::vector<std::string> den(t->n_templates);
     for (int32_t i = 0; i < t->n_templates; ++i) {
-        std::ostringstream acc;
-        acc << "a = 0; ";
-        for (; e < p.prog.size() && p.prog[e].tpl == i; ++e) {
-            const Entry& en = p.prog[e];
-            if (en.mask == 0xFFFFFFFFu) acc << "ACCF(" << en.dword << "); ";
-            else acc << "ACC(" << en.dword << ", 0x" << std::hex << en.mask << std::dec << "); ";
-        }
         const int32_t base = (int32_t)t->lf_size[i] - (int32_t)t->fields_set_size[i];
-        std::ostringstream den;
-        den << "d = dn(" << base << ", " << t->length_slack[i] << ", " << t->length[i] << ", wf, lf); ";
-        const int cc = t->is_cc[i] ? 1 : 0;
-        body << "{ u32 a; i32 d; " << acc.str() << den.str();
-        if (cc) body << "if (!cc) ";
-        body << "{ if ((!FASTV && bi < 0) || ge<FASTV>(a, d, bo, bd)) { bi = " << i
-             << "; bo = a; bd = d; } } }\n";
-        mbody << "{ u32 a; i32 d; " << acc.str() << den.str() << "MOFFER(" << i << ", " << cc << ") }\n";
+        std::ostringstream d;
+        d << "d = dn(" << base << ", " << t->length_slack[i] << ", " << t->length[i] << ", wf, lf); ";
+        den[i] = d.str();
     }
-    s << "#define PROGRAM(FASTV_) { constexpr bool FASTV = FASTV_; \\\n";
-    std::string b = body.str();
-    // one macro line per statement
-    std::istringstream lines(b);
-    std::string line;
-    while (std::getline(lines, line)) s << line << " \\\n";
-    s << "}\n";
+    auto offer = [&](int32_t i) {
+        std::ostringstream o;
+        if (t->is_cc[i]) o << "if (!cc) ";
+        o << "{ if ((!FASTV && bi < 0) || ge<FASTV>(a, d, bo, bd)) { bi = " << i << "; bo = a; bd = d; } }";
+        return o.str();
+    };
+    std::ostringstream match_body, matrix_body, prologue;
+    if (order == 't') {
+        prologue << "u32 f[WQ * 4];\n_Pragma(\"unroll\") for (int q = 0; q < WQ; ++q) { const uint4 v = fp[q * 64]; "
+                    "f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w; }\n";
+        size_t e = 0;
+        for (int32_t i = 0; i < t->n_templates; ++i) {
+            std::ostringstream acc;
+            acc << "a = 0; ";
+            for (; e < p.prog.size() && p.prog[e].tpl == i; ++e) {
+                const Entry& en = p.prog[e];
+                if (en.mask == 0xFFFFFFFFu) acc << "ACCF(" << en.dword << "); ";
+                else acc << "ACC(" << en.dword << ", 0x" << std::hex << en.mask << std::dec << "); ";
+            }
+            match_body << "{ u32 a; i32 d; " << acc.str() << den[i] << offer(i) << " }\n";
+            matrix_body << "{ u32 a; i32 d; " << acc.str() << den[i] << "MOFFER(" << i << ", "
+                        << (t->is_cc[i] ? 1 : 0) << ") }\n";
+        }
+    } else {
+        std::vector<Entry> dm(p.prog);
+        std::stable_sort(dm.begin(), dm.end(), [](const Entry& x, const Entry& y) {
+            return x.dword != y.dword ? x.dword < y.dword : x.tpl < y.tpl;
+        });
+        prologue << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = 0;\n";
+        // quads the program touches, in order; a ring of `pd` registers prefetches quad i+pd
+        // while quad i is consumed; sched_barrier pins each load where it is issued.
+        std::vector<int32_t> quads;
+        for (const Entry& en : dm)
+            if (quads.empty() || quads.back() != en.dword / 4) quads.push_back(en.dword / 4);
+        const char* pd_env = getenv("DICE_PROG_PREFETCH");
+        int pd = pd_env && *pd_env ? atoi(pd_env) : 8;
+        pd = std::max(1, std::min<int>(pd, (int)quads.size()));
+        for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = fp[" << quads[i] * 64 << "];\n";
+        prologue << "__builtin_amdgcn_sched_barrier(0);\n";
+        size_t e = 0;
+        for (size_t qi = 0; qi < quads.size(); ++qi) {
+            const int32_t q = quads[qi];
+            const int slot = (int)(qi % pd);
+            prologue << "{ const uint4 v = pf" << slot << ";";
+            if (qi + pd < quads.size())
+                prologue << " pf" << slot << " = fp[" << quads[qi + pd] * 64 << "]; __builtin_amdgcn_sched_barrier(0);";
+            prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
+            for (; e < dm.size() && dm[e].dword / 4 == q; ++e) {
+                const Entry& en = dm[e];
+                prologue << "acc[" << en.tpl << "] = __builtin_popcount(f[" << en.dword % 4 << "]";
+                if (en.mask != 0xFFFFFFFFu) prologue << " & 0x" << std::hex << en.mask << std::dec << "u";
+                prologue << ") + acc[" << en.tpl << "];\n";
+            }
+            prologue << "}\n";
+        }
+        // persistent form: quad positions padded to a multiple of pd so ring slots line up
+        // across tiles; positions >= nq only prefetch the next tile.
+        {
+            const size_t nq = quads.size();
+            const size_t nqp = ((nq + pd - 1) / pd) * pd;
+            std::ostringstream pp, ps;
+            for (int i = 0; i < pd; ++i) pp << "uint4 pf" << i << " = fp[" << quads[i] * 64 << "];\n";
+            ps << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = 0;\n";
+            size_t e2 = 0;
+            for (size_t qi = 0; qi < nqp; ++qi) {
+                const int slot = (int)(qi % pd);
+                const size_t tgt = qi + pd;
+                ps << "{ ";
+                if (qi < nq) ps << "const uint4 v = pf" << slot << "; ";
+                if (tgt < nq) ps << "pf" << slot << " = fp[" << quads[tgt] * 64 << "]; ";
+                else if (tgt >= nqp) ps << "if (has_next) pf" << slot << " = np[" << quads[tgt - nqp] * 64 << "]; ";
+                ps << "__builtin_amdgcn_sched_barrier(0);";
+                if (qi < nq) {
+                    ps << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
+                    for (; e2 < dm.size() && dm[e2].dword / 4 == quads[qi]; ++e2) {
+                        const Entry& en = dm[e2];
+                        ps << "acc[" << en.tpl << "] = __builtin_popcount(f[" << en.dword % 4 << "]";
+                        if (en.mask != 0xFFFFFFFFu) ps << " & 0x" << std::hex << en.mask << std::dec << "u";
+                        ps << ") + acc[" << en.tpl << "];\n";
+                    }
+                }
+                ps << "}\n";
+            }
+            emit_macro(s, "PERSIST_PROLOGUE", pp.str());
+            emit_macro(s, "PERSIST_STREAM", ps.str());
+        }
+        for (int32_t i = 0; i < t->n_templates; ++i) {
+            match_body << "{ const u32 a = acc[" << i << "]; i32 d; " << den[i] << offer(i) << " }\n";
+            matrix_body << "{ const u32 a = acc[" << i << "]; i32 d; " << den[i] << "MOFFER(" << i << ", "
+                        << (t->is_cc[i] ? 1 : 0) << ") }\n";
+        }
+    }
+    emit_macro(s, "FILE_PROLOGUE", prologue.str());
+    emit_macro(s, "MATCH_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", match_body.str() + "}");
     s << kMatchKernel;
+    if (order == 'd') s << kMatchPersistKernel;
     s << kMatrixOffer;
-    s << "#define MATRIX_PROGRAM(FASTV_) { constexpr bool FASTV = FASTV_; \\\n";
-    std::istringstream ml(mbody.str());
-    while (std::getline(ml, line)) s << line << " \\\n";
-    s << "}\n";
+    emit_macro(s, "MATRIX_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", matrix_body.str() + "}");
     for (int km : {4, 16}) {
         s << "#define KM " << km << "\n#define KNAME dice_prog_matrix" << km << "\n" << kMatrixKernel
           << "#undef KM\n#undef KNAME\n";
@@ -306,6 +448,18 @@ static int compile_or_load(dice_ctx* c, const std::string& src) {
     int rc = compile_cached(src, code, nullptr);
     if (rc != DICE_OK) return rc;
     if (hipModuleLoadData(&c->module, code.data()) != hipSuccess) return fail(DICE_E_DEVICE, "hipModuleLoadData failed");
+    c->prog_match_p = nullptr;
+    if (hipModuleGetFunction(&c->prog_match_p, c->module, "dice_prog_match_p") != hipSuccess) c->prog_match_p = nullptr;
+    (void)hipGetLastError();
+    if (c->prog_match_p) {
+        int nb = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, c->prog_match_p, 256, 0) != hipSuccess) nb = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) prop.multiProcessorCount = 0;
+        c->persist_waves = (int64_t)nb * prop.multiProcessorCount * 4;
+        const char* pe = getenv("DICE_PROG_PERSIST");
+        c->use_persist = pe && *pe == '1' && c->persist_waves > 0;
+    }
     if (hipModuleGetFunction(&c->prog_match, c->module, "dice_prog_match") != hipSuccess ||
         hipModuleGetFunction(&c->prog_matrix, c->module, "dice_prog_matrix4") != hipSuccess ||
         hipModuleGetFunction(&c->prog_matrix16, c->module, "dice_prog_matrix16") != hipSuccess)
@@ -348,10 +502,18 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
 
 int program_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + 63) / 64;
-    const unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    hipFunction_t fn = c->prog_match;
+    if (c->use_persist) {
+        // as many resident waves as needed for equal tile counts per wave
+        const int64_t rounds = (n_tiles + c->persist_waves - 1) / c->persist_waves;
+        const int64_t waves = (n_tiles + rounds - 1) / rounds;
+        grid = (unsigned)((waves + 3) / 4);
+        fn = c->prog_match_p;
+    }
     int64_t n = b->n;
     void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score};
-    if (hipModuleLaunchKernel(c->prog_match, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+    if (hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
         return fail(DICE_E_DEVICE, "launch dice_prog_match failed");
     return DICE_OK;
 }

@@ -11,3 +11,6 @@ struct uint4 { unsigned x, y, z, w; };
 struct Dim3 { unsigned x; };
 static Dim3 threadIdx, blockIdx;
 static inline bool __all(bool v) { return v; }
+#define __builtin_amdgcn_sched_barrier(x) ((void)0)
+struct GridDim { unsigned x; };
+static GridDim gridDim = {1};

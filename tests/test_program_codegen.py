@@ -51,7 +51,8 @@ def run_host(corpus, fb, k, tmp_path):
         fh.write(src)
     shutil.copy(os.path.join(HERE, 'codegen', 'host_shim.h'), d)
     exe = os.path.join(d, 'drv')
-    subprocess.run(['g++', '-O1', '-std=c++17', '-w', '-I', d, '-o', exe, os.path.join(HERE, 'codegen', 'driver.cpp')],
+    defs = ['-DHAS_PERSIST'] if 'dice_prog_match_p' in src else []
+    subprocess.run(['g++', '-O1', '-std=c++17', '-w', '-I', d] + defs + ['-o', exe, os.path.join(HERE, 'codegen', 'driver.cpp')],
                    check=True)
     wq = (corpus.w64 + 1) // 2
     n = fb.n
@@ -81,7 +82,7 @@ def test_generated_program_matches_oracle(tmp_path, k):
 
     templates = License.all(hidden=True, pseudo=False)
     corpus = TemplateCorpus(templates)
-    files = make_files(templates, 150, 21) + [NormFile(''), NormFile('x' * 10, cc=True)]
+    files = make_files(templates, 600, 21) + [NormFile(''), NormFile('x' * 10, cc=True)]
     fb = corpus.intern_files(files)
     best, ov, score, mov, msc, tki, tks = run_host(corpus, fb, k, tmp_path)
     orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
