@@ -1,0 +1,180 @@
+"""GPU tests of the product path against the reference's goldens and at full BASELINE size.
+
+  * Dice matcher API (matchers.Dice over the HIP matrix kernel) on the
+    dice_matcher_spec.rb goldens: exact floats 100.0 / 94.56967213114754 / 26.821370750134918.
+  * LicenseFile#license chain (Copyright -> Exact -> Dice on GPU) on the fixtures.yml cases
+    and on every vendored_license_spec.rb property case.
+  * 1,000,000 synthetic files (BASELINE config 2 size): bit-exact vs the C oracle on a
+    sample, plus size-independent properties over all files (idempotence, match/top-k
+    consistency, top-k sortedness, CC filter).
+  * Dense kernel at T = 600 synthetic templates (config 3 regime) vs the C oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from licensee_amd.license import License
+from licensee_amd.project_files import LicenseFile
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def golden(name):
+    with open(os.path.join(GOLDEN, name), encoding='utf-8') as fh:
+        return json.load(fh)
+
+
+class GoldenLicenseFile(LicenseFile):
+    """A LicenseFile whose normalized content comes from a golden vector (the raw text never
+    leaves the build container); Copyright sees no raw content."""
+
+    def __init__(self, rec):
+        super().__init__('', 'LICENSE')
+        self._content_normalized = rec['normalized']
+        self._fp = rec['cc_false_positive']
+
+    def potential_false_positive(self):
+        return self._fp
+
+
+def test_dice_matcher_spec():
+    from licensee_amd.matchers import Dice
+    cases = golden('dice_spec.json')['cases']
+    d = Dice(GoldenLicenseFile(cases['gpl']['file']))
+    assert [[l.key, s] for l, s in d.matches_by_similarity()[:3]] == cases['gpl']['by_similarity']
+    assert d.match().key == 'gpl-3.0' and d.confidence() == 100.0
+    for name in ('not_a_license', 'stacked', 'cc_nd'):
+        d = Dice(GoldenLicenseFile(cases[name]['file']))
+        assert d.match() is None and d.matches() == [] and d.confidence() == 0 and type(d.confidence()) is int
+    lf = GoldenLicenseFile(cases['cc_by']['file'])
+    assert lf.license().key == 'cc-by-4.0'
+    # LicenseFile#license / #confidence (license_file.rb:92-98, project_file.rb:74-76)
+    # the rendered GPL's wordset equals the template's, so the chain stops at Exact (exact.rb:6-12)
+    lf = GoldenLicenseFile(cases['gpl']['file'])
+    assert lf.license().key == 'gpl-3.0' and lf.confidence() == 100 and lf.matcher().name == 'exact'
+    lf = GoldenLicenseFile(cases['stacked']['file'])
+    assert lf.license().key == 'other' and lf.matcher() is None
+    lf = GoldenLicenseFile(cases['not_a_license']['file'])
+    assert lf.license().key == 'other' and lf.confidence() is None
+    # License#similarity routed through the GPU (content_helper.rb:128-133)
+    agpl = License.find('agpl-3.0')
+    assert agpl.similarity(GoldenLicenseFile(cases['gpl']['file'])) == 94.56967213114754
+    mit = License.find('mit')
+    assert mit.similarity(mit) == 100.0
+
+
+def test_fixture_expectations_on_gpu():
+    recs = golden('fixture_files.json')
+    singles = [r for r in recs if sum(x['fixture'] == r['fixture'] for x in recs) == 1
+               and 'unsupported' not in r and not r['copyright']]
+    for r in singles:
+        exp = r['expected']
+        lf = GoldenLicenseFile(r)
+        key = lf.license().key
+        m = lf.matcher()
+        if exp.get('matcher') in ('dice', 'exact'):
+            assert (key, m.name) == (exp['key'], exp['matcher']), r['fixture']
+        elif exp.get('key') == 'other':
+            assert key == 'other' and m is None, r['fixture']
+
+
+def test_vendored_properties_batched_on_gpu():
+    from licensee_amd.dice import default_engine
+    eng = default_engine()
+    files, expect, keys = [], [], []
+    for t in golden('vendored.json')['templates']:
+        for name, rec in t['cases'].items():
+            files.append(GoldenLicenseFile(rec))
+            expect.append(rec['detected'])
+            keys.append(t['key'])
+    exact = [next((l.key for l in License.all(hidden=True, pseudo=False) if l.wordset() == f.wordset()), None)
+             for f in files]
+    dice = eng.match_files(files, 98)
+    for i in range(len(files)):
+        got = exact[i] or (dice[i][0].key if dice[i][0] is not None else 'other')
+        assert (got == keys[i]) == expect[i], (keys[i], i, got)
+
+
+@pytest.fixture(scope='module')
+def big():
+    from licensee_amd._native import Scorer
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    fb = SyntheticCorpus(corpus).generate(0, 1_000_000, seed=20250202, nthreads=16)
+    sc = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
+                corpus.is_cc, corpus.n_vocab, device=0)
+    batch = sc.batch(fb.n)
+    batch.upload(fb)
+    yield corpus, fb, sc, batch
+    batch.close()
+    sc.close()
+
+
+def test_full_size_match_vs_oracle_sample(big):
+    from oracle.native import OracleScorer
+    corpus, fb, sc, batch = big
+    batch.match(98.0)
+    best, ov, score = batch.download_match()
+    batch.match(98.0)
+    best2, ov2, score2 = batch.download_match()
+    assert np.array_equal(best, best2) and np.array_equal(ov, ov2) and np.array_equal(score, score2)
+    orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                       corpus.length, corpus.is_cc, corpus.n_vocab)
+    idx = np.random.default_rng(1).choice(fb.n, 100_000, replace=False)
+    idx.sort()
+    eb, eo, es = orc.match(fb.bits[idx], fb.wordset_size[idx], fb.length[idx], fb.cc_false_positive[idx], 98.0,
+                           nthreads=16, mode=1)
+    assert np.array_equal(best[idx], eb) and np.array_equal(ov[idx], eo) and np.array_equal(score[idx], es)
+    assert ((best >= 0) == (score >= 98.0)).all()
+    assert best.min() >= -1 and best.max() < len(corpus.templates)
+
+
+def test_full_size_matrix_consistency(big):
+    corpus, fb, sc, batch = big
+    k = 3
+    batch.match(98.0)
+    best, ov, score = batch.download_match()
+    batch.matrix(k)
+    mov, msc, tki, tks = batch.download_matrix(k)
+    rows = np.arange(fb.n)
+    # top-1 of the matrix kernel is the argmax of the match kernel
+    assert np.array_equal(tks[:, 0], score)
+    assert np.array_equal(np.where(tks[:, 0] >= 98.0, tki[:, 0], -1), best)
+    assert np.array_equal(mov[rows, tki[:, 0]], ov)
+    # sorted best-first and consistent with the full matrix
+    assert (tks[:, 0] >= tks[:, 1]).all() and (tks[:, 1] >= tks[:, 2]).all()
+    for j in range(k):
+        assert np.array_equal(msc[rows, tki[:, j]], tks[:, j])
+    # CC filter: flagged files never rank a cc-* template
+    cc_t = np.nonzero(corpus.is_cc)[0]
+    flagged = fb.cc_false_positive.astype(bool)
+    assert not np.isin(tki[flagged], cc_t).any()
+
+
+def test_dense_kernel_600_templates():
+    from licensee_amd._native import Scorer
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    from licensee_amd.synth_templates import synthetic_templates
+    from oracle.native import OracleScorer
+    tpl = synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=5)
+    corpus = TemplateCorpus(tpl)
+    fb = SyntheticCorpus(corpus).generate(0, 3000, seed=11, nthreads=8)
+    sc = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
+                corpus.is_cc, corpus.n_vocab, device=0)
+    assert sc.info()[2] == 0   # dense kernel for T > 64
+    orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                       corpus.length, corpus.is_cc, corpus.n_vocab)
+    best, ov, score = sc.match(fb, 98.0)
+    eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=16)
+    assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+    mov, msc, tki, tks = sc.matrix(fb, 5)
+    emov, emsc = orc.matrix(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, nthreads=16)
+    assert np.array_equal(mov, emov) and np.array_equal(msc, emsc)
+    assert np.array_equal(tks[:, 0], score)
+    assert np.array_equal(np.where(tks[:, 0] >= 98.0, tki[:, 0], -1), best)
+    sc.close()
