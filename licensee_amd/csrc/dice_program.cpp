@@ -57,6 +57,15 @@ __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { u32 r; asm("v_sad_u32 %0,
 __device__ __forceinline__ u32 mul24(u32 a, u32 b) { return (a & 0xffffffu) * (b & 0xffffffu); }
 __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { return a > b ? a - b : b - a; }
 #endif
+// acc += popcount(x & MASK): v_and_b32 (literal) + v_bcnt_u32_b32 accumulate. Written as asm
+// (ACC_ASM) because the compiler otherwise rebalances the chains into v_bcnt(x, 0) + v_add3.
+#if defined(__HIP_DEVICE_COMPILE__) && ACC_ASM
+#define ACCM(acc, x, MASK) { u32 t_; asm("v_and_b32 %1, " #MASK ", %2\n\tv_bcnt_u32_b32 %0, %1, %0" : "+v"(acc), "=&v"(t_) : "v"(x)); }
+#define ACCF1(acc, x) asm("v_bcnt_u32_b32 %0, %1, %0" : "+v"(acc) : "v"(x))
+#else
+#define ACCM(acc, x, MASK) acc = __builtin_popcount((x) & (MASK)) + acc
+#define ACCF1(acc, x) acc = __builtin_popcount(x) + acc
+#endif
 // Denominator (content_helper.rb:130-132,337-347); lengths are non-negative (len_F < 2^31).
 __device__ __forceinline__ i32 dn(i32 base, i32 slack, i32 tlen, u32 wf, i32 lf) {
     const i32 d = (i32)absdiff((u32)tlen, (u32)lf);
@@ -265,6 +274,16 @@ static void build_entries(const dice_templates* t, int32_t w64, Program& p) {
     }
 }
 
+// One dword-major accumulation statement.
+static std::string acc_stmt(const Entry& en) {
+    std::ostringstream o;
+    if (en.mask == 0xFFFFFFFFu)
+        o << "ACCF1(acc[" << en.tpl << "], f[" << en.dword % 4 << "]);\n";
+    else
+        o << "ACCM(acc[" << en.tpl << "], f[" << en.dword % 4 << "], 0x" << std::hex << en.mask << std::dec << ");\n";
+    return o.str();
+}
+
 // Emits `text` as the body of a one-line-per-statement macro.
 static void emit_macro(std::ostringstream& s, const std::string& head, const std::string& text) {
     s << "#define " << head << " \\\n";
@@ -291,6 +310,8 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     s << "#define MATCH_WAVES " << (waves && *waves ? std::string(", ") + waves : std::string()) << "\n";
     uint32_t max_lf = 0;
     for (int32_t i = 0; i < t->n_templates; ++i) max_lf = std::max(max_lf, t->lf_size[i]);
+    const char* acc_asm = getenv("DICE_PROG_ACC_ASM");
+    s << "#define ACC_ASM " << ((acc_asm && *acc_asm == '0') ? 0 : 1) << "\n";
     s << "#define WQ " << wq << "\n#define NT " << t->n_templates << "\n#define CORPUS_FAST "
       << (corpus_fast ? 1 : 0) << "\n#define NARROW_MUL " << (max_lf < (1u << 11) ? 1 : 0) << "\n" << kPrelude;
 
@@ -348,12 +369,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             if (qi + pd < quads.size())
                 prologue << " pf" << slot << " = fp[" << quads[qi + pd] * 64 << "]; __builtin_amdgcn_sched_barrier(0);";
             prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-            for (; e < dm.size() && dm[e].dword / 4 == q; ++e) {
-                const Entry& en = dm[e];
-                prologue << "acc[" << en.tpl << "] = __builtin_popcount(f[" << en.dword % 4 << "]";
-                if (en.mask != 0xFFFFFFFFu) prologue << " & 0x" << std::hex << en.mask << std::dec << "u";
-                prologue << ") + acc[" << en.tpl << "];\n";
-            }
+            for (; e < dm.size() && dm[e].dword / 4 == q; ++e) prologue << acc_stmt(dm[e]);
             prologue << "}\n";
         }
         // persistent form: quad positions padded to a multiple of pd so ring slots line up
@@ -375,12 +391,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
                 ps << "__builtin_amdgcn_sched_barrier(0);";
                 if (qi < nq) {
                     ps << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                    for (; e2 < dm.size() && dm[e2].dword / 4 == quads[qi]; ++e2) {
-                        const Entry& en = dm[e2];
-                        ps << "acc[" << en.tpl << "] = __builtin_popcount(f[" << en.dword % 4 << "]";
-                        if (en.mask != 0xFFFFFFFFu) ps << " & 0x" << std::hex << en.mask << std::dec << "u";
-                        ps << ") + acc[" << en.tpl << "];\n";
-                    }
+                    for (; e2 < dm.size() && dm[e2].dword / 4 == quads[qi]; ++e2) ps << acc_stmt(dm[e2]);
                 }
                 ps << "}\n";
             }
