@@ -73,7 +73,8 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
+    distributed = 'RANK' in os.environ and 'MASTER_PORT' in os.environ   # launched by torch.distributed.run
+    if distributed:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         torch.cuda.set_device(local_rank)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
@@ -91,7 +92,9 @@ def main():
     synth = SyntheticCorpus(corpus, profile=1 if cfg == 4 else 0)
     nthreads = min(16, os.cpu_count() or 1)
     t0 = time.time()
-    files = synth.generate(rank * n_per, n_per, seed=20250202, nthreads=nthreads)
+    from licensee_amd.shard import shard_range
+    first, count = shard_range(rank, world, n_per)
+    files = synth.generate(first, count, seed=20250202, nthreads=nthreads)
     log(f'rank {rank}: generated {n_per} files in {time.time() - t0:.1f}s (V={corpus.n_vocab}, T={len(templates)})')
 
     scorer = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
@@ -115,7 +118,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -126,12 +129,12 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
     ev_ms = ev0.elapsed_time(ev1)
-    if world > 1:
+    if distributed:
         t = torch.tensor([wall, ev_ms], dtype=torch.float64, device='cuda')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, ev_ms = float(t[0]), float(t[1])
@@ -167,7 +170,7 @@ def main():
         host_gather_s = time.perf_counter() - t_g
         extras['host_gather_ms'] = host_gather_s * 1e3
         extras['matches'] = int((best >= 0).sum())
-        if world > 1:
+        if distributed:
             # RCCL alternative: all_gather the 16-B/file results over xGMI
             res = torch.empty((n_per, 4), dtype=torch.int32, device='cuda')
             hip = ctypes.CDLL('libamdhip64.so')
@@ -194,6 +197,24 @@ def main():
             extras['host_gather_ms'] = float(t[0]) * 1e3
             extras['rccl_allgather_ms'] = float(t[1]) * 1e3
             extras['gather_winner'] = 'host' if t[0] <= t[1] else 'rccl'
+
+    # ---- separately reported rates (never `value`): PCIe-inclusive end-to-end, host prep ----
+    if rank == 0 and cfg != 5 and not args.probe:
+        torch.cuda.synchronize()
+        t_e = time.perf_counter()
+        batch.upload(files, sptr)
+        batch.match(args.threshold, sptr)
+        batch.download_match(sptr)
+        extras['e2e_pcie_files_per_s'] = n_per / (time.perf_counter() - t_e)
+        from licensee_amd.project_files import LicenseFile
+        sample = [synth.text(i)[0] for i in range(200)]
+        t_h = time.perf_counter()
+        prepped = [LicenseFile(txt, 'LICENSE') for txt in sample]
+        for lf in prepped:
+            lf.content_normalized()
+        corpus.intern_files(prepped)
+        extras['host_prep_files_per_s'] = len(sample) / (time.perf_counter() - t_h)
+        extras['host_prep_note'] = 'Python normalize+intern, 1 thread, 200 synthetic texts (SURVEY 8f row 1: C++ next)'
 
     cpu_baseline = None
     parity = None
@@ -257,7 +278,7 @@ def main():
             'extras': extras,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -115,6 +115,8 @@ void dice_batch_destroy(dice_batch *batch);
 int dice_batch_upload(dice_batch *batch, const dice_files *files, void *stream);
 /* Kernel-only scoring of the resident batch (asynchronous on `stream`). */
 int dice_batch_match(dice_batch *batch, double threshold, void *stream);
+/* Device-resident matrix results are template-major ([T][n] overlap/score, [k][n] top-k) so
+ * every store is coalesced; dice_batch_download_matrix returns them row-major. */
 int dice_batch_matrix(dice_batch *batch, int32_t k, void *stream);
 /* D2H of results (synchronizes `stream`); NULL outputs are skipped. */
 int dice_batch_download_match(dice_batch *batch, int32_t *best, uint32_t *overlap,

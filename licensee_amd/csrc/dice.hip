@@ -57,6 +57,25 @@ __global__ __launch_bounds__(256) void dice_pack_tiles(const uint64_t* __restric
     tiles[gid] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 
+// [rows][cols] -> [cols][rows] through a padded 64x64 LDS tile (element size 4 or 8 bytes).
+// Used to hand the template-major device matrix back in the ABI's row-major [n][T] layout.
+template <class E>
+__global__ __launch_bounds__(256) void dice_transpose(const E* __restrict__ src, E* __restrict__ dst,
+                                                     int64_t rows, int64_t cols) {
+    __shared__ E tile[64][65];
+    const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t r = r0 + i, c = c0 + tx;
+        if (r < rows && c < cols) tile[i][tx] = src[r * cols + c];
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t c = c0 + i, r = r0 + tx;
+        if (r < rows && c < cols) dst[c * rows + r] = tile[tx][i];
+    }
+}
+
 // Diagnostic: pure streaming read of the resident tile layout (same addresses and widths as
 // the scorers, trivial compute, 16 B written per file). Measures the read ceiling that the
 // Dice kernels are judged against (DESIGN.md "roofline").
@@ -76,8 +95,15 @@ __global__ __launch_bounds__(256) void dice_stream_probe(const uint4* __restrict
     if (file < n) out[file] = x;
 }
 
-__device__ __forceinline__ uint32_t popc_and4(uint4 f, uint4 m) {
-    return __popc(f.x & m.x) + __popc(f.y & m.y) + __popc(f.z & m.z) + __popc(f.w & m.w);
+// acc += popcount(f & m) over a quad: v_and_b32 (template dword from an SGPR) + v_bcnt_u32_b32
+// accumulate, 8 VALU per quad (the compiler's own form, v_bcnt(x, 0) + v_add3 trees, is 10).
+__device__ __forceinline__ void acc_and4(uint32_t& acc, uint4 f, uint4 m) {
+    uint32_t t0, t1, t2, t3;
+    asm("v_and_b32 %1, %5, %9\n\tv_and_b32 %2, %6, %10\n\tv_and_b32 %3, %7, %11\n\tv_and_b32 %4, %8, %12\n\t"
+        "v_bcnt_u32_b32 %0, %1, %0\n\tv_bcnt_u32_b32 %0, %2, %0\n\tv_bcnt_u32_b32 %0, %3, %0\n\t"
+        "v_bcnt_u32_b32 %0, %4, %0"
+        : "+v"(acc), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+        : "s"(m.x), "s"(m.y), "s"(m.z), "s"(m.w), "v"(f.x), "v"(f.y), "v"(f.z), "v"(f.w));
 }
 
 // Dense scorer: any T, any V. Templates are uniform across the wave, so the compiler keeps
@@ -108,7 +134,7 @@ __global__ __launch_bounds__(256) void dice_dense_match(
         for (int q = 0; q < wq; ++q) {
             const uint4 f = fp[(int64_t)q * kWave];
 #pragma unroll
-            for (int j = 0; j < TT; ++j) acc[j] += popc_and4(f, mrow[j]);
+            for (int j = 0; j < TT; ++j) acc_and4(acc[j], f, mrow[j]);
             mrow += tpad;
         }
 #pragma unroll
@@ -188,7 +214,7 @@ __global__ __launch_bounds__(256) void dice_dense_matrix(
         for (int q = 0; q < wq; ++q) {
             const uint4 f = fp[(int64_t)q * kWave];
 #pragma unroll
-            for (int j = 0; j < TT; ++j) acc[j] += popc_and4(f, mrow[j]);
+            for (int j = 0; j < TT; ++j) acc_and4(acc[j], f, mrow[j]);
             mrow += tpad;
         }
 #pragma unroll
@@ -198,8 +224,8 @@ __global__ __launch_bounds__(256) void dice_dense_matrix(
                 const int4 c = tc[t];
                 const int32_t den = dice_den(c, my_wf, my_len);
                 if (valid) {
-                    if (ov_out) ov_out[file * T + t] = acc[j];
-                    if (score_out) score_out[file * T + t] = dice_score(acc[j], den);
+                    if (ov_out) ov_out[(int64_t)t * n + file] = acc[j];   // template-major [T][n]
+                    if (score_out) score_out[(int64_t)t * n + file] = dice_score(acc[j], den);
                 }
                 if (!(c.w && my_cc)) top.offer(t, acc[j], den);
             }
@@ -209,8 +235,8 @@ __global__ __launch_bounds__(256) void dice_dense_matrix(
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             if (j < k) {
-                topk_idx[file * k + j] = top.idx[j];
-                topk_score[file * k + j] = top.idx[j] >= 0 ? dice_score(top.ov[j], top.den[j]) : -1.0;
+                topk_idx[(int64_t)j * n + file] = top.idx[j];
+                topk_score[(int64_t)j * n + file] = top.idx[j] >= 0 ? dice_score(top.ov[j], top.den[j]) : -1.0;
             }
         }
     }
@@ -255,6 +281,26 @@ int dalloc(T** p, size_t count) {
 }  // namespace
 
 static hipStream_t pick_stream(dice_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+
+template <class E>
+static int transpose_to_host(dice_batch* b, const E* d_src, int64_t rows, int64_t cols, E* host, hipStream_t s) {
+    // rows x cols (template-major) -> cols x rows on device, then D2H
+    const size_t bytes = (size_t)rows * cols * sizeof(E);
+    if (b->stage_bytes < bytes) {
+        if (b->d_stage) (void)hipFree(b->d_stage);
+        b->d_stage = nullptr;
+        b->stage_bytes = 0;
+        if (hipMalloc(&b->d_stage, bytes) != hipSuccess) return fail(DICE_E_NOMEM, "stage alloc");
+        b->stage_bytes = bytes;
+    }
+    dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+    hipLaunchKernelGGL(dice_transpose<E>, grid, dim3(256), 0, s, d_src, (E*)b->d_stage, rows, cols);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(host, b->d_stage, bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return DICE_OK;
+}
+
 
 extern "C" {
 
@@ -350,8 +396,8 @@ int dice_ctx_info(const dice_ctx* ctx, int32_t* T, int32_t* V, int32_t* kind, in
 void dice_batch_destroy(dice_batch* b) {
     if (!b) return;
     DeviceGuard g(b->ctx->device);
-    void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf, b->d_len, b->d_cc, b->d_best,
-                    b->d_ov,   b->d_score, b->d_mov, b->d_mscore, b->d_tki, b->d_tks};
+    void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,  b->d_best, b->d_ov,
+                    b->d_score, b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -502,15 +548,14 @@ int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32
     dice_ctx* c = b->ctx;
     DeviceGuard g(c->device);
     hipStream_t s = pick_stream(c, stream);
-    const size_t n = (size_t)b->n;
+    const int64_t n = b->n;
     if (n && !b->d_mov) return fail(DICE_E_STATE, "dice_batch_matrix was not run");
-    if (n) {
-        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_mov, n * c->T * 4, hipMemcpyDeviceToHost, s));
-        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_mscore, n * c->T * 8, hipMemcpyDeviceToHost, s));
-        if (tki && b->k_used) HIP_TRY(hipMemcpyAsync(tki, b->d_tki, n * b->k_used * 4, hipMemcpyDeviceToHost, s));
-        if (tks && b->k_used) HIP_TRY(hipMemcpyAsync(tks, b->d_tks, n * b->k_used * 8, hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipStreamSynchronize(s));
+    if (!n) return DICE_OK;
+    int rc;
+    if (ov && (rc = transpose_to_host<uint32_t>(b, b->d_mov, c->T, n, ov, s))) return rc;
+    if (score && (rc = transpose_to_host<double>(b, b->d_mscore, c->T, n, score, s))) return rc;
+    if (tki && b->k_used && (rc = transpose_to_host<int32_t>(b, b->d_tki, b->k_used, n, tki, s))) return rc;
+    if (tks && b->k_used && (rc = transpose_to_host<double>(b, b->d_tks, b->k_used, n, tks, s))) return rc;
     return DICE_OK;
 }
 

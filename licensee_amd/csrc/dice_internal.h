@@ -56,8 +56,10 @@ struct dice_batch {
     int64_t mat_cap = 0;
     int32_t mat_k = 0;
     int32_t k_used = 0;
-    uint32_t* d_mov = nullptr;
-    double* d_mscore = nullptr;
+    uint32_t* d_mov = nullptr;      // template-major [T][capacity] (coalesced stores)
+    double* d_mscore = nullptr;     // template-major [T][capacity]
     int32_t* d_tki = nullptr;
     double* d_tks = nullptr;
+    void* d_stage = nullptr;        // row-major staging for downloads
+    size_t stage_bytes = 0;
 };

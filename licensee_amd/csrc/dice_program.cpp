@@ -182,8 +182,9 @@ extern "C" __global__ __launch_bounds__(256) void KNAME(
     i32 ti[KM]; u32 to[KM]; i32 td[KM];
 #pragma unroll
     for (int j = 0; j < KM; ++j) { ti[j] = -1; to[j] = 0; td[j] = 1; }
-    u32* orow = ov_out ? ov_out + file * NT : nullptr;
-    double* srow = score_out ? score_out + file * NT : nullptr;
+    // template-major [NT][n] outputs: for a fixed template the 64 lanes store contiguously
+    u32* orow = ov_out ? ov_out + file : nullptr;
+    double* srow = score_out ? score_out + file : nullptr;
     if (__all(fast)) {
         MATRIX_BODY(true)
     } else {
@@ -193,8 +194,8 @@ extern "C" __global__ __launch_bounds__(256) void KNAME(
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             if (j < k) {
-                topk_idx[file * k + j] = ti[j];
-                topk_score[file * k + j] = ti[j] >= 0 ? sc(to[j], td[j]) : -1.0;
+                topk_idx[(i64)j * n + file] = ti[j];
+                topk_score[(i64)j * n + file] = ti[j] >= 0 ? sc(to[j], td[j]) : -1.0;
             }
         }
     }
@@ -207,7 +208,7 @@ extern "C" __global__ __launch_bounds__(256) void KNAME(
 const char* kMatrixOffer = R"HIP(
 #define MOFFER(T, CCF)                                                                  \
     {                                                                                   \
-        if (valid) { if (orow) orow[T] = a; if (srow) srow[T] = sc(a, d); }            \
+        if (valid) { if (orow) orow[(i64)(T) * n] = a; if (srow) srow[(i64)(T) * n] = sc(a, d); } \
         if (!((CCF) && cc)) {                                                           \
             int p = 0;                                                                  \
             _Pragma("unroll") for (int j = 0; j < KM; ++j)                              \

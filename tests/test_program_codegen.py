@@ -67,8 +67,9 @@ def run_host(corpus, fb, k, tmp_path):
     T = corpus.lf_bits.shape[0]
     rd = lambda name, dt: np.fromfile(os.path.join(d, name), dt)
     return (rd('best.out', np.int32), rd('ov.out', np.uint32), rd('score.out', np.float64),
-            rd('mov.out', np.uint32).reshape(n, T), rd('msc.out', np.float64).reshape(n, T),
-            rd('tki.out', np.int32).reshape(n, max(k, 1))[:, :k], rd('tks.out', np.float64).reshape(n, max(k, 1))[:, :k])
+            # device matrix layout is template-major: [T][n] and [k][n]
+            rd('mov.out', np.uint32).reshape(T, n).T, rd('msc.out', np.float64).reshape(T, n).T,
+            rd('tki.out', np.int32).reshape(max(k, 1), n)[:k].T, rd('tks.out', np.float64).reshape(max(k, 1), n)[:k].T)
 
 
 @pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
