@@ -1,0 +1,53 @@
+/*
+ * licensee_host.h -- C-ABI of the native host preparation library (liblicensee_host.so).
+ *
+ * Host side of the Dice path: turns raw license files into the
+ * dice_files inputs of licensee_dice.h, in host threads. Replaces, for bulk use:
+ *   ProjectFile#initialize decode + universal newline   lib/licensee/project_files/project_file.rb:37-45
+ *   ContentHelper#content_normalized / #wordset          lib/licensee/content_helper.rb:108-110,144-168,219-321
+ *   LicenseFile#potential_false_positive?                lib/licensee/project_files/license_file.rb:80-82
+ *   Matchers::Copyright#match                            lib/licensee/matchers/copyright.rb:12-17
+ *   Matchers::Exact#match                                lib/licensee/matchers/exact.rb:6-12
+ * The regular expressions are supplied by the caller (licensee_amd/content_helper.py passes
+ * its compiled patterns), so host paths share one pattern source. Texts outside the native
+ * envelope (non-ASCII letters, HTML) report status 1 and are prepared by the caller.
+ */
+#ifndef LICENSEE_HOST_H
+#define LICENSEE_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lh_ctx lh_ctx;
+
+/* Patterns (name, Python-re source, re flags I|M|S), the spelling map and the vocabulary
+ * (word id = position). Returns NULL and writes err on failure. */
+lh_ctx *lh_create(int32_t n_patterns, const char *const *names, const char *const *patterns,
+                  const int32_t *flags, int32_t n_spell, const char *const *spell_from,
+                  const char *const *spell_to, int32_t n_vocab, const char *const *vocab,
+                  char *err, int32_t errcap);
+void lh_destroy(lh_ctx *ctx);
+
+/* Exact-matcher data: [T][words64(V)] Lf bitsets, |wordset| and the field words. */
+int lh_set_templates(lh_ctx *ctx, int32_t n_templates, const uint64_t *lf_bits,
+                     const uint32_t *wordset_size, const int32_t *field_off,
+                     const char *const *field_words);
+
+/* content_normalized of one text (UTF-8 out); -1 = outside the native envelope. */
+int64_t lh_normalize(lh_ctx *ctx, const char *data, int64_t len, const char *filename,
+                     int32_t is_file, char *out, int64_t cap);
+
+/* Batched preparation of n LicenseFiles into dice_files arrays + matcher flags. */
+int lh_prep_files(lh_ctx *ctx, int64_t n, const char *const *data, const int64_t *lens,
+                  const char *const *filenames, int32_t nthreads, uint64_t *bits, uint32_t *wf,
+                  int32_t *length, uint8_t *cc, uint8_t *copyright, int32_t *exact,
+                  uint8_t *status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LICENSEE_HOST_H */

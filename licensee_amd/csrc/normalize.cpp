@@ -1,0 +1,419 @@
+// Native host normalizer + interner: licensee's
+// ContentHelper#content_normalized (lib/licensee/content_helper.rb:144-168, 219-321) and
+// #wordset (:108-110), the LicenseFile decode (project_file.rb:37-45), the Copyright matcher
+// (copyright.rb:12-17), the Exact matcher (exact.rb:6-12) and potential_false_positive?
+// (license_file.rb:80-82), batched over host threads.
+//
+// The op sequence mirrors licensee_amd/content_helper.py one for one; the regular
+// expressions themselves are handed over from that module's compiled patterns at lh_create
+// time and run on rx (rx.h), so both host paths share a single pattern source.
+// Texts containing characters whose Python case mapping or \b / \w semantics could differ
+// from the ASCII rules implemented here (non-ASCII letters/digits) -- and HTML files -- are
+// reported as status 1 and normalized by the Python path instead.
+#include <malloc.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "rx.h"
+
+using rx::Regex;
+using rx::Str;
+
+namespace {
+
+const char32_t kSpace = U' ';
+
+bool is_strip_char(char32_t c) { return c == 0 || c == ' ' || (c >= '\t' && c <= '\r'); }
+
+Str ruby_strip(const Str& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && is_strip_char(s[a])) ++a;
+    while (b > a && is_strip_char(s[b - 1])) --b;
+    return s.substr(a, b - a);
+}
+
+Str squeeze_spaces(const Str& s) {
+    Str out;
+    out.reserve(s.size());
+    for (size_t i = 0; i < s.size(); ++i) {
+        if (s[i] == kSpace && !out.empty() && out.back() == kSpace) continue;
+        out.push_back(s[i]);
+    }
+    return out;
+}
+
+bool contains(const Str& s, const char* lit) {
+    Str l = rx::from_utf8(lit);
+    return s.find(l) != Str::npos;
+}
+
+// non-ASCII code points whose Python semantics match the ASCII rules used here: no case
+// mapping, not \w (str.isalnum() is False) -- punctuation, symbols, spaces, BOM.
+bool safe_nonascii(char32_t c) {
+    if (c >= 0xA0 && c <= 0xBF) return !(c == 0xAA || c == 0xB2 || c == 0xB3 || c == 0xB5 || c == 0xB9 || c == 0xBA ||
+                                         (c >= 0xBC && c <= 0xBE));
+    if (c == 0xD7 || c == 0xF7) return true;
+    if (c >= 0x2000 && c <= 0x206F) return true;   // general punctuation
+    if (c >= 0x20A0 && c <= 0x20CF) return true;   // currency
+    if (c >= 0x2190 && c <= 0x22FF) return true;   // arrows, math operators
+    if (c >= 0x2500 && c <= 0x25FF) return true;   // box drawing, blocks, shapes
+    if (c == 0xFEFF || c == 0xFFFD || c == 0x3000) return true;
+    return false;
+}
+
+struct Ctx {
+    std::map<std::string, Regex> re;
+    std::vector<std::pair<Str, Str>> spell;
+    std::unordered_map<std::string, int32_t> vocab;
+    int32_t n_vocab = 0, w64 = 0;
+    // templates (Exact)
+    int32_t n_templates = 0;
+    std::vector<uint64_t> lf_bits;                  // [T][w64]
+    std::vector<uint32_t> full_size;                // |wordset|
+    std::vector<std::vector<std::string>> fields;   // field words in the wordset
+    std::string err;
+
+    const Regex& R(const char* name) const { return re.at(name); }
+};
+
+struct Normalizer {
+    const Ctx& c;
+    Str cur;
+
+    void strip_re(const Regex& r) { cur = ruby_strip(squeeze_spaces(r.sub(cur, U" "))); }
+    void sub_re(const Regex& r, const char32_t* repl) { cur = r.sub(cur, Str(repl)); }
+
+    void strip_title() {
+        const Regex& t = c.R("title");
+        std::vector<long> caps;
+        while (t.search(cur, 0, caps)) strip_re(t);
+    }
+    void strip_copyright() {
+        const Regex& t = c.R("strip_copyright");
+        std::vector<long> caps;
+        while (t.search(cur, 0, caps)) strip_re(t);
+    }
+    void strip_comments() {
+        // String#split("\n") drops trailing empty fields
+        std::vector<Str> lines;
+        size_t a = 0;
+        for (size_t i = 0; i <= cur.size(); ++i) {
+            if (i == cur.size() || cur[i] == '\n') { lines.push_back(cur.substr(a, i - a)); a = i + 1; }
+        }
+        while (!lines.empty() && lines.back().empty()) lines.pop_back();
+        if (lines.size() == 1) return;
+        std::vector<long> caps;
+        const Regex& cm = c.R("comment_markup");
+        for (auto& l : lines)
+            if (!cm.search(l, 0, caps)) return;
+        strip_re(cm);
+    }
+
+    // hyphenated (content_helper.rb:40) can only match a '-' followed by [ \t\v\f\r]* and '\n'
+    static bool has_hyphen_break(const Str& s) {
+        for (size_t i = 0; i < s.size(); ++i) {
+            if (s[i] != '-') continue;
+            size_t j = i + 1;
+            while (j < s.size() && (s[j] == ' ' || s[j] == '\t' || s[j] == '\v' || s[j] == '\f' || s[j] == '\r')) ++j;
+            if (j < s.size() && s[j] == '\n') return true;
+        }
+        return false;
+    }
+
+    // normalize_spelling (content_helper.rb:314-316): /\b(?:k1|k2|...)\b/ with ordered
+    // alternatives, tried only where \b can hold before a letter (a word start); text on this
+    // path has ASCII word characters only, so \b is the ASCII boundary.
+    void spelling() {
+        Str out;
+        out.reserve(cur.size());
+        const size_t n = cur.size();
+        size_t i = 0;
+        auto word = [](char32_t ch) { return (ch >= 'a' && ch <= 'z') || (ch >= 'A' && ch <= 'Z') || (ch >= '0' && ch <= '9') || ch == '_'; };
+        while (i < n) {
+            if (word(cur[i]) && (i == 0 || !word(cur[i - 1]))) {
+                bool hit = false;
+                for (auto& kv : c.spell) {
+                    const Str& k = kv.first;
+                    if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 &&
+                        (i + k.size() == n || !word(cur[i + k.size()]))) {
+                        out += kv.second;
+                        i += k.size();
+                        hit = true;
+                        break;
+                    }
+                }
+                if (hit) continue;
+            }
+            out.push_back(cur[i++]);
+        }
+        cur.swap(out);
+    }
+
+    // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip
+    void collapse_whitespace() {
+        Str out;
+        out.reserve(cur.size());
+        for (char32_t ch : cur) {
+            const bool ws = ch == ' ' || (ch >= '\t' && ch <= '\r');
+            if (ws) { if (out.empty() || out.back() != ' ') out.push_back(' '); }
+            else out.push_back(ch);
+        }
+        cur = ruby_strip(out);
+    }
+
+    // content_without_title_and_version + content_normalized (content_helper.rb:144-168)
+    Str run(const Str& content) {
+        cur = ruby_strip(content);
+        strip_re(c.R("hrs"));
+        strip_comments();
+        strip_re(c.R("markdown_headings"));
+        sub_re(c.R("link_markup"), U"\\1");
+        strip_title();
+        strip_re(c.R("version"));
+        for (auto& ch : cur)
+            if (ch >= 'A' && ch <= 'Z') ch += 32;
+        sub_re(c.R("lists"), U"- \\1");
+        sub_re(c.R("https"), U"https:");
+        {   // '&' -> 'and'
+            Str out;
+            for (char32_t ch : cur) {
+                if (ch == '&') out += U"and";
+                else out.push_back(ch);
+            }
+            cur.swap(out);
+        }
+        sub_re(c.R("dashes"), U"-");
+        sub_re(c.R("quote"), U"'");
+        if (has_hyphen_break(cur)) sub_re(c.R("hyphenated"), U"\\1-\\2");
+        spelling();
+        sub_re(c.R("span_markup"), U"\\1");
+        sub_re(c.R("bullet"), U"\n\n- ");
+        sub_re(c.R("bullet_paren"), U")(");
+        // STRIP_METHODS (content_helper.rb:89-105)
+        strip_re(c.R("bom"));
+        if (contains(cur, "creative commons")) { strip_re(c.R("cc_dedication")); strip_re(c.R("cc_wiki")); }
+        if (contains(cur, "associating cc0")) {
+            strip_re(c.R("cc_legal_code")); strip_re(c.R("cc0_info")); strip_re(c.R("cc0_disclaimer"));
+        }
+        if (contains(cur, "unlicense")) strip_re(c.R("unlicense_info"));
+        sub_re(c.R("border_markup"), U"\\1");
+        strip_title();
+        strip_re(c.R("version"));
+        strip_re(c.R("url"));
+        strip_copyright();
+        strip_title();
+        strip_re(c.R("block_markup"));
+        strip_re(c.R("developed_by"));
+        {
+            std::vector<long> caps;
+            if (c.R("end_of_terms").search(cur, 0, caps)) cur.resize((size_t)caps[0]);
+        }
+        collapse_whitespace();
+        strip_re(c.R("mit_optional"));
+        return cur;
+    }
+};
+
+// wordset scan (content_helper.rb:109): (?:[\w/-](?:'s|(?<=s)')?)+ with ASCII \w
+inline bool wchar(char32_t c) {
+    return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_' || c == '/' || c == '-';
+}
+
+template <class F>
+void scan_words(const Str& s, F&& emit) {
+    size_t i = 0;
+    const size_t n = s.size();
+    while (i < n) {
+        if (!wchar(s[i])) { ++i; continue; }
+        const size_t a = i;
+        while (i < n && wchar(s[i])) {
+            const char32_t ch = s[i++];
+            if (i + 1 < n + 1 && i < n && s[i] == '\'') {
+                if (i + 1 < n && s[i + 1] == 's') i += 2;
+                else if (ch == 's') i += 1;
+            }
+        }
+        emit(a, i);
+    }
+}
+
+bool extname_is_html(const char* fn) {
+    if (!fn) return false;
+    std::string base(fn);
+    size_t sl = base.rfind('/');
+    if (sl != std::string::npos) base = base.substr(sl + 1);
+    size_t st = base.find_first_not_of('.');
+    if (st == std::string::npos) return false;
+    std::string rest = base.substr(st);
+    size_t dot = rest.rfind('.');
+    if (dot == std::string::npos) return false;
+    std::string ext = rest.substr(dot);
+    for (auto& ch : ext) ch = (char)tolower((unsigned char)ch);
+    return ext.find(".htm") != std::string::npos;   // /\.html?/i.match?(extname)
+}
+
+struct FileOut {
+    int status = 0;      // 0 ok, 1 needs the Python path, 2 error
+    Str normalized;
+    bool cc = false, copyright = false;
+};
+
+void prep_one(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o) {
+    Str content = rx::from_utf8(std::string(data, (size_t)len));
+    if (is_file) {   // universal newline (project_file.rb:41)
+        Str t;
+        t.reserve(content.size());
+        for (size_t i = 0; i < content.size(); ++i) {
+            if (content[i] == '\r') {
+                t.push_back('\n');
+                if (i + 1 < content.size() && content[i + 1] == '\n') ++i;
+            } else t.push_back(content[i]);
+        }
+        content.swap(t);
+    }
+    for (char32_t ch : content)
+        if (ch >= 0x80 && !safe_nonascii(ch)) { o.status = 1; return; }
+    if (extname_is_html(filename)) { o.status = 1; return; }
+    std::vector<long> caps;
+    const Str stripped = ruby_strip(content);
+    o.cc = c.R("cc_false_positive").search(stripped, 0, caps);
+    o.copyright = c.R("copyright_match").search(stripped, 0, caps);
+    Normalizer nz{c, Str()};
+    o.normalized = nz.run(content);
+}
+
+}  // namespace
+
+extern "C" {
+
+typedef struct lh_ctx lh_ctx;
+
+lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* const* patterns, const int32_t* flags,
+                  int32_t n_spell, const char* const* spell_from, const char* const* spell_to, int32_t n_vocab,
+                  const char* const* vocab, char* err, int32_t errcap) {
+    // every normalization pass allocates a text-sized buffer (~4 B/char, often near glibc's
+    // 128 KiB mmap threshold): keep them in the per-thread arenas instead of mmap/munmap
+    // churn, which serializes the batch threads on the kernel's mm lock.
+    mallopt(M_MMAP_THRESHOLD, 64 << 20);
+    mallopt(M_TRIM_THRESHOLD, 128 << 20);
+    Ctx* c = new Ctx();
+    try {
+        for (int32_t i = 0; i < n_patterns; ++i) c->re.emplace(names[i], Regex(patterns[i], flags[i]));
+        for (int32_t i = 0; i < n_spell; ++i) c->spell.push_back({rx::from_utf8(spell_from[i]), rx::from_utf8(spell_to[i])});
+        for (int32_t i = 0; i < n_vocab; ++i) c->vocab.emplace(vocab[i], i);
+        c->n_vocab = n_vocab;
+        c->w64 = (n_vocab + 63) / 64;
+        const char* need[] = {"hrs", "comment_markup", "markdown_headings", "link_markup", "title", "version",
+                              "lists", "https", "dashes", "quote", "hyphenated", "spelling", "span_markup",
+                              "bullet", "bullet_paren", "bom", "cc_dedication", "cc_wiki", "cc_legal_code",
+                              "cc0_info", "cc0_disclaimer", "unlicense_info", "border_markup", "url",
+                              "strip_copyright", "block_markup", "developed_by", "end_of_terms", "whitespace",
+                              "mit_optional", "cc_false_positive", "copyright_match"};
+        for (const char* nm : need)
+            if (!c->re.count(nm)) throw std::runtime_error(std::string("missing pattern ") + nm);
+    } catch (const std::exception& e) {
+        if (err && errcap > 0) snprintf(err, (size_t)errcap, "%s", e.what());
+        delete c;
+        return nullptr;
+    }
+    return reinterpret_cast<lh_ctx*>(c);
+}
+
+void lh_destroy(lh_ctx* ctx) { delete reinterpret_cast<Ctx*>(ctx); }
+
+// Exact matcher data: template Lf bitsets over the vocabulary, |wordset| and field words
+// (Lf ∪ fields = wordset, content_helper.rb:323-335).
+int lh_set_templates(lh_ctx* ctx, int32_t n_templates, const uint64_t* lf_bits, const uint32_t* wordset_size,
+                     const int32_t* field_off, const char* const* field_words) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    c->n_templates = n_templates;
+    c->lf_bits.assign(lf_bits, lf_bits + (size_t)n_templates * c->w64);
+    c->full_size.assign(wordset_size, wordset_size + n_templates);
+    c->fields.assign(n_templates, {});
+    for (int32_t t = 0; t < n_templates; ++t)
+        for (int32_t k = field_off[t]; k < field_off[t + 1]; ++k) c->fields[t].push_back(field_words[k]);
+    return 0;
+}
+
+// Normalize one text. Returns UTF-8 byte count written to out (NUL-terminated when room),
+// the needed size when cap is too small, -1 when the text needs the Python path.
+int64_t lh_normalize(lh_ctx* ctx, const char* data, int64_t len, const char* filename, int32_t is_file, char* out,
+                     int64_t cap) {
+    const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+    FileOut o;
+    prep_one(*c, data, len, filename, is_file != 0, o);
+    if (o.status) return -1;
+    const std::string u = rx::to_utf8(o.normalized);
+    if (out && cap > (int64_t)u.size()) {
+        memcpy(out, u.data(), u.size());
+        out[u.size()] = 0;
+    }
+    return (int64_t)u.size();
+}
+
+// Batched LicenseFile preparation: decode, normalize, wordset scan, intern to the vocabulary
+// bitset, |W_F|, len_F, CC flag, Copyright and Exact matchers.
+//   status[i]: 0 ok; 1 the caller must use the Python path for file i (its outputs unset).
+//   exact[i]:  first template (key order) whose wordset equals the file's, or -1.
+int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t* lens, const char* const* filenames,
+                  int32_t nthreads, uint64_t* bits, uint32_t* wf, int32_t* length, uint8_t* cc, uint8_t* copyright,
+                  int32_t* exact, uint8_t* status) {
+    const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+    if (nthreads < 1) nthreads = 1;
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        std::vector<uint64_t> row((size_t)c->w64);
+        for (;;) {
+            const int64_t i = next.fetch_add(16);
+            if (i >= n) break;
+            for (int64_t f = i; f < std::min<int64_t>(n, i + 16); ++f) {
+                FileOut o;
+                prep_one(*c, data[f], lens[f], filenames ? filenames[f] : nullptr, true, o);
+                status[f] = (uint8_t)o.status;
+                if (o.status) continue;
+                std::fill(row.begin(), row.end(), 0);
+                std::unordered_set<std::string> words;
+                std::string w;
+                scan_words(o.normalized, [&](size_t a, size_t b) {
+                    w.clear();
+                    for (size_t k = a; k < b; ++k) w.push_back((char)o.normalized[k]);   // ASCII only
+                    if (words.insert(w).second) {
+                        auto it = c->vocab.find(w);
+                        if (it != c->vocab.end()) row[(size_t)it->second >> 6] |= 1ULL << (it->second & 63);
+                    }
+                });
+                memcpy(bits + (size_t)f * c->w64, row.data(), sizeof(uint64_t) * (size_t)c->w64);
+                wf[f] = (uint32_t)words.size();
+                length[f] = (int32_t)o.normalized.size();
+                cc[f] = o.cc;
+                copyright[f] = o.copyright;
+                int32_t ex = -1;
+                for (int32_t t = 0; t < c->n_templates && ex < 0; ++t) {
+                    if (c->full_size[t] != words.size()) continue;
+                    const uint64_t* L = c->lf_bits.data() + (size_t)t * c->w64;
+                    bool ok = true;
+                    for (int32_t k = 0; k < c->w64 && ok; ++k) ok = (row[k] & L[k]) == L[k];
+                    for (size_t k = 0; k < c->fields[t].size() && ok; ++k) ok = words.count(c->fields[t][k]) > 0;
+                    if (ok) ex = t;
+                }
+                exact[f] = ex;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int32_t t = 0; t < nthreads; ++t) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,516 @@
+// Backtracking regex engine for the Python `re` subset of licensee_amd/content_helper.py.
+// See rx.h for the supported syntax. Semantics follow Python's sre: leftmost match,
+// ordered alternation, greedy / lazy quantifiers with backtracking, fixed-width lookbehind.
+#include "rx.h"
+
+#include <stdexcept>
+
+namespace rx {
+
+// ---- UTF-8 ---------------------------------------------------------------------------
+// UTF-8 -> code points with Python's errors='ignore' semantics: an invalid sequence's
+// maximal valid prefix (at least one byte) is dropped (project_file.rb:38-40 replace: '').
+Str from_utf8(const std::string& s) {
+    Str out;
+    out.reserve(s.size());
+    const size_t n = s.size();
+    size_t i = 0;
+    auto byte = [&](size_t k) { return (unsigned)(unsigned char)s[k]; };
+    while (i < n) {
+        const unsigned c = byte(i);
+        if (c < 0x80) { out.push_back(c); ++i; continue; }
+        int need;
+        unsigned lo = 0x80, hi = 0xBF;   // allowed range of the first continuation byte
+        char32_t cp;
+        if (c >= 0xC2 && c <= 0xDF) { need = 1; cp = c & 0x1F; }
+        else if (c == 0xE0) { need = 2; lo = 0xA0; cp = c & 0x0F; }
+        else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) { need = 2; cp = c & 0x0F; }
+        else if (c == 0xED) { need = 2; hi = 0x9F; cp = c & 0x0F; }
+        else if (c == 0xF0) { need = 3; lo = 0x90; cp = c & 0x07; }
+        else if (c >= 0xF1 && c <= 0xF3) { need = 3; cp = c & 0x07; }
+        else if (c == 0xF4) { need = 3; hi = 0x8F; cp = c & 0x07; }
+        else { ++i; continue; }
+        size_t k = 1;
+        bool ok = true;
+        for (; k <= (size_t)need; ++k) {
+            if (i + k >= n) { ok = false; break; }
+            const unsigned b = byte(i + k);
+            const unsigned l = k == 1 ? lo : 0x80, h = k == 1 ? hi : 0xBF;
+            if (b < l || b > h) { ok = false; break; }
+            cp = (cp << 6) | (b & 0x3F);
+        }
+        if (!ok) { i += k; continue; }   // drop the maximal subpart
+        out.push_back(cp);
+        i += need + 1;
+    }
+    return out;
+}
+
+std::string to_utf8(const Str& s) {
+    std::string out;
+    out.reserve(s.size());
+    for (char32_t c : s) {
+        if (c < 0x80) out.push_back((char)c);
+        else if (c < 0x800) { out.push_back((char)(0xC0 | (c >> 6))); out.push_back((char)(0x80 | (c & 0x3F))); }
+        else if (c < 0x10000) {
+            out.push_back((char)(0xE0 | (c >> 12)));
+            out.push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+            out.push_back((char)(0x80 | (c & 0x3F)));
+        } else {
+            out.push_back((char)(0xF0 | (c >> 18)));
+            out.push_back((char)(0x80 | ((c >> 12) & 0x3F)));
+            out.push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+            out.push_back((char)(0x80 | (c & 0x3F)));
+        }
+    }
+    return out;
+}
+
+static inline char32_t fold(char32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+static inline bool is_word(char32_t c) {
+    return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+}
+
+// ---- parser ----------------------------------------------------------------------------
+struct Parser {
+    Str p;
+    size_t i = 0;
+    int ngroups = 0;
+
+    [[noreturn]] void err(const char* m) { throw std::runtime_error(std::string("rx parse: ") + m); }
+    bool eof() const { return i >= p.size(); }
+    char32_t peek() const { return p[i]; }
+
+    NodeP mk(Node::Kind k) { auto n = std::make_shared<Node>(); n->kind = k; return n; }
+
+    char32_t hex(int n) {
+        char32_t v = 0;
+        for (int k = 0; k < n; ++k) {
+            if (eof()) err("short hex escape");
+            char32_t c = p[i++];
+            v = v * 16 + (c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : (err("bad hex"), 0));
+        }
+        return v;
+    }
+
+    // an escaped literal character (inside or outside classes); -1 if it is a class/anchor
+    long escape_char(char32_t c) {
+        switch (c) {
+            case 'n': return '\n';
+            case 't': return '\t';
+            case 'v': return '\v';
+            case 'f': return '\f';
+            case 'r': return '\r';
+            case 'u': return (long)hex(4);
+            case 'x': return (long)hex(2);
+            default:
+                if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9')) return -1;
+                return (long)c;
+        }
+    }
+
+    NodeP parse_alt(bool icase, bool dotall) {
+        auto alt = mk(Node::ALT);
+        alt->kids.push_back(parse_seq(icase, dotall));
+        while (!eof() && peek() == '|') {
+            ++i;
+            alt->kids.push_back(parse_seq(icase, dotall));
+        }
+        return alt->kids.size() == 1 ? alt->kids[0] : alt;
+    }
+
+    NodeP parse_seq(bool icase, bool dotall) {
+        auto seq = mk(Node::SEQ);
+        while (!eof() && peek() != '|' && peek() != ')') {
+            NodeP a = parse_atom(icase, dotall);
+            if (!a) continue;
+            seq->kids.push_back(parse_quant(a));
+        }
+        return seq;
+    }
+
+    NodeP parse_quant(NodeP a) {
+        while (!eof()) {
+            int mn, mx;
+            char32_t c = peek();
+            if (c == '*') { mn = 0; mx = -1; ++i; }
+            else if (c == '+') { mn = 1; mx = -1; ++i; }
+            else if (c == '?') { mn = 0; mx = 1; ++i; }
+            else if (c == '{') {
+                size_t save = i++;
+                auto num = [&](int& out) { bool any = false; out = 0; while (!eof() && peek() >= '0' && peek() <= '9') { out = out * 10 + (int)(peek() - '0'); ++i; any = true; } return any; };
+                int a1 = 0, a2 = 0;
+                bool h1 = num(a1);
+                if (!eof() && peek() == '}') { ++i; if (!h1) { i = save; return a; } mn = mx = a1; }
+                else if (!eof() && peek() == ',') {
+                    ++i;
+                    bool h2 = num(a2);
+                    if (eof() || peek() != '}') { i = save; return a; }
+                    ++i;
+                    mn = h1 ? a1 : 0;
+                    mx = h2 ? a2 : -1;
+                } else { i = save; return a; }
+            } else break;
+            auto r = mk(Node::REPEAT);
+            r->min = mn; r->max = mx;
+            if (!eof() && peek() == '?') { r->lazy = true; ++i; }
+            r->kids.push_back(a);
+            a = r;
+        }
+        return a;
+    }
+
+    NodeP parse_class(bool icase) {
+        auto c = mk(Node::CLASS);
+        c->icase = icase;
+        if (!eof() && peek() == '^') { c->negate = true; ++i; }
+        bool first = true;
+        while (!eof() && (peek() != ']' || first)) {
+            first = false;
+            char32_t lo = p[i++];
+            if (lo == '\\') {
+                if (eof()) err("bad class escape");
+                long e = escape_char(p[i++]);
+                if (e < 0) err("unsupported class escape");
+                lo = (char32_t)e;
+            }
+            char32_t hi = lo;
+            if (i + 1 < p.size() && peek() == '-' && p[i + 1] != ']') {
+                ++i;
+                hi = p[i++];
+                if (hi == '\\') {
+                    long e = escape_char(p[i++]);
+                    if (e < 0) err("unsupported class escape");
+                    hi = (char32_t)e;
+                }
+            }
+            c->ranges.push_back({lo, hi});
+        }
+        if (eof()) err("unterminated class");
+        ++i;
+        return c;
+    }
+
+    NodeP parse_atom(bool icase, bool dotall) {
+        char32_t c = p[i++];
+        switch (c) {
+            case '.': { auto n = mk(Node::ANY); n->dotall = dotall; return n; }
+            case '^': return mk(Node::BOL);
+            case '$': return mk(Node::EOL);
+            case '[': return parse_class(icase);
+            case '(': {
+                if (!eof() && peek() == '?') {
+                    ++i;
+                    if (eof()) err("bad group");
+                    char32_t k = p[i];
+                    if (k == ':') { ++i; auto g = mk(Node::GROUP); g->kids.push_back(parse_alt(icase, dotall)); close(); return g; }
+                    if (k == '=' || k == '!') {
+                        ++i;
+                        auto l = mk(Node::LOOK); l->negate = k == '!';
+                        l->kids.push_back(parse_alt(icase, dotall)); close(); return l;
+                    }
+                    if (k == '<' && i + 1 < p.size() && (p[i + 1] == '=' || p[i + 1] == '!')) {
+                        auto l = mk(Node::LOOK); l->behind = true; l->negate = p[i + 1] == '!';
+                        i += 2;
+                        l->kids.push_back(parse_alt(icase, dotall)); close();
+                        l->width = width(l->kids[0]);
+                        if (l->width < 0) err("lookbehind requires fixed width");
+                        return l;
+                    }
+                    // scoped flags (?i:...) (?-i:...) (?s:...)
+                    bool on = true, ic = icase, da = dotall;
+                    while (!eof() && peek() != ':') {
+                        char32_t f = p[i++];
+                        if (f == '-') on = false;
+                        else if (f == 'i') ic = on;
+                        else if (f == 's') da = on;
+                        else if (f == 'm' || f == 'x' || f == 'u') {}
+                        else err("unsupported flag");
+                    }
+                    if (eof()) err("bad flags group");
+                    ++i;
+                    auto g = mk(Node::GROUP); g->kids.push_back(parse_alt(ic, da)); close(); return g;
+                }
+                auto g = mk(Node::GROUP);
+                g->group = ++ngroups;
+                g->kids.push_back(parse_alt(icase, dotall));
+                close();
+                return g;
+            }
+            case '\\': {
+                if (eof()) err("trailing backslash");
+                char32_t e = p[i++];
+                if (e == 'A') return mk(Node::BOS);
+                if (e == 'Z') return mk(Node::EOS);
+                if (e == 'b') return mk(Node::WORDB);
+                long v = escape_char(e);
+                if (v < 0) err("unsupported escape");
+                auto n = mk(Node::LIT); n->ch = (char32_t)v; n->icase = icase; return n;
+            }
+            default: { auto n = mk(Node::LIT); n->ch = c; n->icase = icase; return n; }
+        }
+    }
+
+    void close() { if (eof() || peek() != ')') err("missing )"); ++i; }
+
+    static int width(const NodeP& n) {
+        switch (n->kind) {
+            case Node::LIT: case Node::ANY: case Node::CLASS: return 1;
+            case Node::BOL: case Node::EOL: case Node::BOS: case Node::EOS: case Node::WORDB: case Node::LOOK: return 0;
+            case Node::SEQ: { int w = 0; for (auto& k : n->kids) { int x = width(k); if (x < 0) return -1; w += x; } return w; }
+            case Node::ALT: { int w = -2; for (auto& k : n->kids) { int x = width(k); if (x < 0 || (w != -2 && x != w)) return -1; w = x; } return w < 0 ? 0 : w; }
+            case Node::GROUP: return width(n->kids[0]);
+            case Node::REPEAT: { if (n->min != n->max) return -1; int x = width(n->kids[0]); return x < 0 ? -1 : x * n->min; }
+        }
+        return -1;
+    }
+};
+
+// ---- matcher (continuation passing over the node tree) -------------------------------
+struct Cont {
+    virtual bool operator()(size_t pos) const = 0;
+};
+
+struct Matcher {
+    const Str& s;
+    std::vector<long>& caps;
+
+    bool lit(const Node* n, size_t pos) const {
+        if (pos >= s.size()) return false;
+        char32_t c = s[pos];
+        return n->icase ? fold(c) == fold(n->ch) : c == n->ch;
+    }
+    bool cls(const Node* n, size_t pos) const {
+        if (pos >= s.size()) return false;
+        char32_t c = s[pos];
+        bool in = false;
+        for (auto& r : n->ranges) {
+            if (c >= r.first && c <= r.second) { in = true; break; }
+            if (n->icase) {
+                char32_t f = fold(c), u = (c >= 'a' && c <= 'z') ? c - 32 : c;
+                if ((f >= r.first && f <= r.second) || (u >= r.first && u <= r.second)) { in = true; break; }
+            }
+        }
+        return in != n->negate;
+    }
+
+    // match node n at pos, then continuation k
+    bool m(const Node* n, size_t pos, const Cont& k) {
+        switch (n->kind) {
+            case Node::LIT: return lit(n, pos) && k(pos + 1);
+            case Node::ANY: return pos < s.size() && (n->dotall || s[pos] != '\n') && k(pos + 1);
+            case Node::CLASS: return cls(n, pos) && k(pos + 1);
+            case Node::BOL: return (pos == 0 || s[pos - 1] == '\n') && k(pos);
+            case Node::EOL: return (pos == s.size() || s[pos] == '\n') && k(pos);
+            case Node::BOS: return pos == 0 && k(pos);
+            case Node::EOS: return pos == s.size() && k(pos);
+            case Node::WORDB: {
+                bool a = pos > 0 && is_word(s[pos - 1]), b = pos < s.size() && is_word(s[pos]);
+                return a != b && k(pos);
+            }
+            case Node::SEQ: return seq(n, 0, pos, k);
+            case Node::ALT:
+                for (auto& kid : n->kids)
+                    if (m(kid.get(), pos, k)) return true;
+                return false;
+            case Node::GROUP: {
+                if (n->group < 0) return m(n->kids[0].get(), pos, k);
+                const long o0 = caps[2 * n->group], o1 = caps[2 * n->group + 1];
+                struct C : Cont {
+                    Matcher* self; const Node* n; size_t start; const Cont* k;
+                    bool operator()(size_t e) const override {
+                        const long p0 = self->caps[2 * n->group], p1 = self->caps[2 * n->group + 1];
+                        self->caps[2 * n->group] = (long)start;
+                        self->caps[2 * n->group + 1] = (long)e;
+                        if ((*k)(e)) return true;
+                        self->caps[2 * n->group] = p0;
+                        self->caps[2 * n->group + 1] = p1;
+                        return false;
+                    }
+                } c;
+                c.self = this; c.n = n; c.start = pos; c.k = &k;
+                if (m(n->kids[0].get(), pos, c)) return true;
+                caps[2 * n->group] = o0; caps[2 * n->group + 1] = o1;
+                return false;
+            }
+            case Node::REPEAT: return rep(n, 0, pos, (size_t)-1, k);
+            case Node::LOOK: {
+                bool ok;
+                struct Acc : Cont { size_t want; bool any; bool operator()(size_t e) const override { return any || e == want; } } acc;
+                std::vector<long> save(caps);
+                if (n->behind) {
+                    if (pos < (size_t)n->width) ok = false;
+                    else { acc.want = pos; acc.any = false; ok = m(n->kids[0].get(), pos - n->width, acc); }
+                } else {
+                    acc.any = true; ok = m(n->kids[0].get(), pos, acc);
+                }
+                if (n->negate) { caps = save; return !ok && k(pos); }
+                if (!ok) { caps = save; return false; }
+                return k(pos);
+            }
+        }
+        return false;
+    }
+
+    bool seq(const Node* n, size_t idx, size_t pos, const Cont& k) {
+        if (idx == n->kids.size()) return k(pos);
+        struct C : Cont {
+            Matcher* self; const Node* n; size_t idx; const Cont* k;
+            bool operator()(size_t p) const override { return self->seq(n, idx + 1, p, *k); }
+        } c;
+        c.self = this; c.n = n; c.idx = idx; c.k = &k;
+        return m(n->kids[idx].get(), pos, c);
+    }
+
+    bool single(const Node* n, size_t pos) const {
+        switch (n->kind) {
+            case Node::LIT: return lit(n, pos);
+            case Node::ANY: return pos < s.size() && (n->dotall || s[pos] != '\n');
+            case Node::CLASS: return cls(n, pos);
+            default: return false;
+        }
+    }
+
+    bool rep(const Node* n, int count, size_t pos, size_t last, const Cont& k) {
+        const Node* kid = n->kids[0].get();
+        if (count == 0 && (kid->kind == Node::LIT || kid->kind == Node::ANY || kid->kind == Node::CLASS)) {
+            // one character per iteration: iterate instead of recursing per character
+            size_t run = 0;
+            const size_t cap = n->max < 0 ? (size_t)-1 : (size_t)n->max;
+            if (n->lazy) {
+                while (run < (size_t)n->min) { if (!single(kid, pos + run)) return false; ++run; }
+                for (;;) {
+                    if (k(pos + run)) return true;
+                    if (run >= cap || !single(kid, pos + run)) return false;
+                    ++run;
+                }
+            }
+            while (run < cap && single(kid, pos + run)) ++run;
+            if (run < (size_t)n->min) return false;
+            for (size_t r = run + 1; r-- > (size_t)n->min;)
+                if (k(pos + r)) return true;
+            return false;
+        }
+        const bool can_more = n->max < 0 || count < n->max;
+        const bool can_stop = count >= n->min;
+        struct C : Cont {
+            Matcher* self; const Node* n; int count; size_t start; const Cont* k;
+            bool operator()(size_t p) const override {
+                if (p == start && count >= n->min) return false;   // empty iteration: stop looping
+                return self->rep(n, count + 1, p, start, *k);
+            }
+        } c;
+        c.self = this; c.n = n; c.count = count; c.start = pos; c.k = &k;
+        (void)last;
+        if (n->lazy) {
+            if (can_stop && k(pos)) return true;
+            return can_more && m(kid, pos, c);
+        }
+        if (can_more && m(kid, pos, c)) return true;
+        return can_stop && k(pos);
+    }
+};
+
+static void first_chars(const NodeP& n, std::vector<bool>& set, bool& nonascii, bool& nullable) {
+    // conservative first-character set of n (ASCII bitmap); nullable = may match empty
+    switch (n->kind) {
+        case Node::LIT:
+            if (n->ch < 128) { set[n->ch] = true; if (n->icase) { set[fold(n->ch)] = true; if (n->ch >= 'a' && n->ch <= 'z') set[n->ch - 32] = true; } }
+            else nonascii = true;
+            nullable = false; return;
+        case Node::ANY: for (int c = 0; c < 128; ++c) set[c] = true; nonascii = true; nullable = false; return;
+        case Node::CLASS:
+            if (n->negate) { for (int c = 0; c < 128; ++c) set[c] = true; nonascii = true; nullable = false; return; }
+            for (auto& r : n->ranges) {
+                for (char32_t c = r.first; c <= r.second && c < 128; ++c) {
+                    set[c] = true;
+                    if (n->icase) { set[fold(c)] = true; if (c >= 'a' && c <= 'z') set[c - 32] = true; }
+                }
+                if (r.second >= 128) nonascii = true;
+            }
+            nullable = false; return;
+        case Node::SEQ: {
+            for (auto& k : n->kids) {
+                bool nl = false;
+                first_chars(k, set, nonascii, nl);
+                if (!nl) { nullable = false; return; }
+            }
+            nullable = true; return;
+        }
+        case Node::ALT: {
+            bool any = false;
+            for (auto& k : n->kids) { bool nl = false; first_chars(k, set, nonascii, nl); any |= nl; }
+            nullable = any; return;
+        }
+        case Node::GROUP: first_chars(n->kids[0], set, nonascii, nullable); return;
+        case Node::REPEAT: { bool nl = false; first_chars(n->kids[0], set, nonascii, nl); nullable = nl || n->min == 0; return; }
+        default: nullable = true; return;   // anchors / lookarounds are zero-width
+    }
+}
+
+Regex::Regex(const std::string& utf8, int flags) {
+    Parser ps;
+    ps.p = from_utf8(utf8);
+    root_ = ps.parse_alt((flags & IGNORECASE) != 0, (flags & DOTALL) != 0);
+    if (!ps.eof()) throw std::runtime_error("rx parse: unbalanced )");
+    ngroups_ = ps.ngroups;
+    // anchored if the first element of the top sequence is \A
+    const Node* r = root_.get();
+    while (r->kind == Node::GROUP && r->group < 0) r = r->kids[0].get();
+    if (r->kind == Node::SEQ && !r->kids.empty()) {
+        const Node* f = r->kids[0].get();
+        while (f->kind == Node::GROUP && f->group < 0) {
+            const Node* g = f->kids[0].get();
+            if (g->kind == Node::SEQ && !g->kids.empty()) f = g->kids[0].get(); else f = g;
+        }
+        anchored_ = f->kind == Node::BOS;
+    }
+    std::vector<bool> set(128, false);
+    bool nonascii = false, nullable = false;
+    first_chars(root_, set, nonascii, nullable);
+    if (!nullable) { first_ = set; first_nonascii_ = nonascii; }
+}
+
+bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
+    caps.assign(2 * (ngroups_ + 1), -1);
+    struct End : Cont { size_t* out; bool operator()(size_t e) const override { *out = e; return true; } } end;
+    size_t e = 0;
+    end.out = &e;
+    Matcher mt{s, caps};
+    for (size_t pos = start; pos <= s.size(); ++pos) {
+        if (anchored_ && pos > 0) return false;
+        if (!first_.empty()) {
+            if (pos == s.size()) return false;
+            char32_t c = s[pos];
+            if (c < 128 ? !first_[c] : !first_nonascii_) continue;
+        }
+        if (mt.m(root_.get(), pos, end)) {
+            caps[0] = (long)pos;
+            caps[1] = (long)e;
+            return true;
+        }
+    }
+    return false;
+}
+
+Str Regex::sub(const Str& s, const Str& repl, bool* changed) const {
+    bool any = false;
+    Str out = sub_fn(s, [&](const Str& src, const std::vector<long>& caps) {
+        any = true;
+        Str r;
+        for (size_t i = 0; i < repl.size(); ++i) {
+            if (repl[i] == '\\' && i + 1 < repl.size() && repl[i + 1] >= '0' && repl[i + 1] <= '9') {
+                int g = (int)(repl[i + 1] - '0');
+                ++i;
+                if (g <= ngroups_ && caps[2 * g] >= 0) r.append(src, (size_t)caps[2 * g], (size_t)(caps[2 * g + 1] - caps[2 * g]));
+            } else {
+                r.push_back(repl[i]);
+            }
+        }
+        return r;
+    });
+    if (changed) *changed = any;
+    return out;
+}
+
+}  // namespace rx

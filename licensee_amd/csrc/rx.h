@@ -1,0 +1,90 @@
+// Minimal backtracking regex engine over UTF-32 code points, implementing exactly the
+// Python `re` subset used by licensee_amd/content_helper.py (the host restatement of
+// lib/licensee/content_helper.rb): literals and escapes (\A \Z \b \n \t \v \f \r \uXXXX and
+// escaped punctuation), classes with ranges / negation, '.', groups (capturing, (?:),
+// scoped flags (?i:) (?-i:)), lookbehind (?<!..) (?<=..) and lookahead (?=..) (?!..) of
+// fixed width, alternation, greedy and lazy quantifiers (* + ? {m,n}), ^ and $ (always
+// multiline here, as every pattern is compiled with re.M). Case-insensitive matching folds
+// ASCII only; callers route text containing non-ASCII letters to the Python path, where
+// Unicode folding could differ (normalize.cpp).
+#pragma once
+
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace rx {
+
+using Str = std::u32string;
+
+enum Flags : int { IGNORECASE = 2, MULTILINE = 8, DOTALL = 16 };  // Python re flag values
+
+struct Node;
+using NodeP = std::shared_ptr<Node>;
+
+struct Node {
+    enum Kind { LIT, ANY, CLASS, SEQ, ALT, GROUP, REPEAT, BOL, EOL, BOS, EOS, WORDB, LOOK };
+    Kind kind;
+    char32_t ch = 0;                                // LIT
+    bool icase = false;                             // LIT / CLASS
+    bool dotall = false;                            // ANY
+    bool negate = false;                            // CLASS, LOOK (negative)
+    bool behind = false;                            // LOOK
+    std::vector<std::pair<char32_t, char32_t>> ranges;  // CLASS
+    std::vector<NodeP> kids;                        // SEQ / ALT / GROUP(1) / REPEAT(1) / LOOK(1)
+    int group = -1;                                 // GROUP capture index (-1: none)
+    int min = 0, max = -1;                          // REPEAT (-1: unbounded)
+    bool lazy = false;                              // REPEAT
+    int width = -1;                                 // LOOK (behind): fixed width
+};
+
+class Regex {
+public:
+    Regex() = default;
+    Regex(const std::string& utf8_pattern, int flags);
+    // search from `start`; on success fills caps ([2*i], [2*i+1]; -1 when unset) for i <= ngroups
+    bool search(const Str& s, size_t start, std::vector<long>& caps) const;
+    int ngroups() const { return ngroups_; }
+    bool anchored() const { return anchored_; }
+    // re.sub with a template supporting \1..\9 (and literal text); count = 0 -> all
+    Str sub(const Str& s, const Str& repl, bool* changed = nullptr) const;
+    template <class F>
+    Str sub_fn(const Str& s, F&& fn) const;  // replacement computed from the match
+    bool valid() const { return (bool)root_; }
+
+private:
+    NodeP root_;
+    int ngroups_ = 0;
+    bool anchored_ = false;           // pattern starts with \A
+    std::vector<bool> first_;         // ASCII first-char filter (empty = any)
+    bool first_nonascii_ = true;
+    friend struct Matcher;
+};
+
+Str from_utf8(const std::string& s);
+std::string to_utf8(const Str& s);
+
+}  // namespace rx
+
+// ---- template implementation ---------------------------------------------------------
+namespace rx {
+template <class F>
+Str Regex::sub_fn(const Str& s, F&& fn) const {
+    Str out;
+    size_t pos = 0, last = 0;
+    std::vector<long> caps;
+    while (pos <= s.size() && search(s, pos, caps)) {
+        const size_t ms = (size_t)caps[0], me = (size_t)caps[1];
+        out.append(s, last, ms - last);
+        out += fn(s, caps);
+        last = me;
+        pos = me > ms ? me : me + 1;
+        if (me == ms && ms < s.size()) out.push_back(s[ms]), last = ms + 1;
+        if (anchored_) break;
+    }
+    if (last < s.size()) out.append(s, last, Str::npos);
+    return out;
+}
+}  // namespace rx

@@ -1,0 +1,151 @@
+"""Native host preparation (licensee_amd/lib/liblicensee_host.so, csrc/normalize.cpp + rx.cpp).
+
+Batched LicenseFile preparation in C++ threads: decode -> content_normalized -> wordset ->
+vocabulary bitset, plus the CC flag, the Copyright matcher and the Exact matcher. The regular
+expressions are exactly the compiled patterns of ``content_helper.py`` (handed over here),
+so the two host paths share one pattern source; texts the native path does not cover
+(non-ASCII letters, HTML) fall back to the Python path per file.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import content_helper as ch
+from ._native import FileBatch
+from .license import License
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib', 'liblicensee_host.so')
+_FLAG_MASK = 2 | 8 | 16   # re.I | re.M | re.S
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        l = ctypes.CDLL(LIB_PATH)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        cpp = ctypes.POINTER(ctypes.c_char_p)
+        l.lh_create.restype = vp
+        l.lh_create.argtypes = [i32, cpp, cpp, vp, i32, cpp, cpp, i32, cpp, ctypes.c_char_p, i32]
+        l.lh_destroy.argtypes = [vp]
+        l.lh_set_templates.restype = ctypes.c_int
+        l.lh_set_templates.argtypes = [vp, i32, vp, vp, vp, cpp]
+        l.lh_normalize.restype = i64
+        l.lh_normalize.argtypes = [vp, ctypes.c_char_p, i64, ctypes.c_char_p, i32, ctypes.c_char_p, i64]
+        l.lh_prep_files.restype = ctypes.c_int
+        l.lh_prep_files.argtypes = [vp, i64, cpp, vp, cpp, i32, vp, vp, vp, vp, vp, vp, vp]
+        _lib = l
+    return _lib
+
+
+def _cstrs(items: Sequence[Union[str, bytes]]):
+    enc = [x if isinstance(x, bytes) else x.encode('utf-8') for x in items]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    return arr, enc
+
+
+def host_patterns():
+    """(name, compiled pattern) pairs the native normalizer runs (content_helper.py)."""
+    from .project_files import CC_FALSE_POSITIVE_REGEX
+    R, N = ch.REGEXES, ch.NORMALIZATIONS
+    pats = {k: R[k] for k in ('hrs', 'comment_markup', 'markdown_headings', 'link_markup', 'version', 'bom',
+                             'cc_dedication', 'cc_wiki', 'cc_legal_code', 'cc0_info', 'cc0_disclaimer',
+                             'unlicense_info', 'border_markup', 'url', 'block_markup', 'developed_by',
+                             'whitespace', 'mit_optional', 'bullet', 'span_markup')}
+    pats.update({k: N[k][0] for k in ('lists', 'https', 'dashes', 'quote', 'hyphenated')})
+    pats.update({'spelling': ch._SPELLING_REGEX, 'bullet_paren': ch._BULLET_PAREN_REGEX,
+                 'end_of_terms': ch.END_OF_TERMS_REGEX, 'strip_copyright': ch._STRIP_COPYRIGHT_REGEX,
+                 'title': License.title_regex(), 'cc_false_positive': CC_FALSE_POSITIVE_REGEX,
+                 'copyright_match': ch.COPYRIGHT_MATCH_REGEX})
+    return pats
+
+
+class HostPrep:
+    def __init__(self, corpus=None):
+        """``corpus``: a TemplateCorpus (vocabulary + Exact data); None = normalize only."""
+        lib = _load()
+        pats = host_patterns()
+        names, self._k1 = _cstrs(list(pats))
+        srcs, self._k2 = _cstrs([p.pattern for p in pats.values()])
+        flags = np.array([p.flags & _FLAG_MASK for p in pats.values()], np.int32)
+        sf, self._k3 = _cstrs(list(ch.VARIETAL_WORDS))
+        st, self._k4 = _cstrs(list(ch.VARIETAL_WORDS.values()))
+        vocab = corpus.vocab if corpus is not None else []
+        vw, self._k5 = _cstrs(vocab)
+        err = ctypes.create_string_buffer(512)
+        self._flags = flags
+        self._c = lib.lh_create(len(pats), names, srcs, flags.ctypes.data, len(ch.VARIETAL_WORDS), sf, st,
+                                len(vocab), vw, err, 512)
+        if not self._c:
+            raise RuntimeError('lh_create failed: ' + err.value.decode())
+        self.corpus = corpus
+        if corpus is not None:
+            tpl = corpus.templates
+            ws = np.array([len(t.wordset()) for t in tpl], np.uint32)
+            fields, off = [], [0]
+            for t in tpl:
+                fs = sorted(set(t.fields_normalized()))
+                fields.extend(fs)
+                off.append(len(fields))
+            fw, self._k6 = _cstrs(fields)
+            self._off = np.array(off, np.int32)
+            self._ws = ws
+            self._lf = np.ascontiguousarray(corpus.lf_bits)
+            lib.lh_set_templates(self._c, len(tpl), self._lf.ctypes.data, ws.ctypes.data, self._off.ctypes.data, fw)
+
+    def __del__(self):
+        if getattr(self, '_c', None):
+            _load().lh_destroy(self._c)
+            self._c = None
+
+    def normalize(self, content: Union[str, bytes], filename: Optional[str] = None, is_file: bool = True) -> Optional[str]:
+        """Native content_normalized, or None when the text needs the Python path."""
+        data = content if isinstance(content, bytes) else content.encode('utf-8')
+        fn = filename.encode('utf-8') if filename else None
+        n = _load().lh_normalize(self._c, data, len(data), fn, 1 if is_file else 0, None, 0)
+        if n < 0:
+            return None
+        buf = ctypes.create_string_buffer(n + 1)
+        _load().lh_normalize(self._c, data, len(data), fn, 1 if is_file else 0, buf, n + 1)
+        return buf.raw[:n].decode('utf-8')
+
+    def prep_files(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
+                   nthreads: int = 8) -> Tuple[FileBatch, np.ndarray, np.ndarray, np.ndarray]:
+        """Returns (FileBatch, copyright flags, exact template index or -1, fell_back mask).
+        Files the native path does not cover are prepared by the Python LicenseFile path."""
+        if self.corpus is None:
+            raise ValueError('prep_files needs a TemplateCorpus')
+        n = len(contents)
+        data, keep = _cstrs(contents)
+        lens = np.array([len(x) for x in keep], np.int64)
+        fns = None
+        if filenames is not None:
+            fns, self._kf = _cstrs(filenames)
+        w64 = self.corpus.w64
+        bits = np.zeros((n, w64), np.uint64)
+        wf = np.zeros(n, np.uint32)
+        ln = np.zeros(n, np.int32)
+        cc = np.zeros(n, np.uint8)
+        cr = np.zeros(n, np.uint8)
+        ex = np.full(n, -1, np.int32)
+        st = np.zeros(n, np.uint8)
+        _load().lh_prep_files(self._c, n, data, lens.ctypes.data, fns, nthreads, bits.ctypes.data, wf.ctypes.data,
+                              ln.ctypes.data, cc.ctypes.data, cr.ctypes.data, ex.ctypes.data, st.ctypes.data)
+        fell = st != 0
+        if fell.any():
+            from .matchers import Copyright, Exact
+            from .project_files import LicenseFile
+            idx = {t.key: i for i, t in enumerate(self.corpus.templates)}
+            for i in np.nonzero(fell)[0]:
+                lf = LicenseFile(contents[i], filenames[i] if filenames is not None else 'LICENSE')
+                bits[i], wf[i] = self.corpus.intern(lf.wordset() or frozenset())
+                ln[i] = lf.length()
+                cc[i] = lf.potential_false_positive()
+                cr[i] = Copyright(lf).match() is not None
+                e = Exact(lf).match()
+                ex[i] = idx.get(e.key, -1) if e is not None else -1
+        return FileBatch(bits, wf, ln, cc), cr.astype(bool), ex, fell

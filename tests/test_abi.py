@@ -12,24 +12,29 @@ from licensee_amd import _native
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
-    names = set()
-    inc = os.path.join(ROOT, 'include')
-    for fn in os.listdir(inc):
-        if fn.endswith('.h'):
-            src = open(os.path.join(inc, fn)).read()
-            src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
-            names |= set(re.findall(r'\b(dice_[a-z0-9_]+)\s*\(', src))
-    return names
+def declared_functions(header, prefix):
+    src = open(os.path.join(ROOT, 'include', header)).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return set(re.findall(r'\b(' + prefix + r'[a-z0-9_]+)\s*\(', src))
 
 
 def test_library_exports_every_declared_symbol():
     lib = _native.load_library()
-    declared = declared_functions()
+    declared = declared_functions('licensee_dice.h', 'dice_')
     assert len(declared) >= 18
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(_native.EXPORTED_SYMBOLS) == declared
+
+
+def test_host_library_exports_every_declared_symbol():
+    from licensee_amd import native_host
+    lib = native_host._load()
+    declared = declared_functions('licensee_host.h', 'lh_')
+    assert declared == {'lh_create', 'lh_destroy', 'lh_set_templates', 'lh_normalize', 'lh_prep_files'}
+    for name in sorted(declared):
+        assert hasattr(lib, name), name
+    assert set(os.listdir(os.path.join(ROOT, 'include'))) == {'licensee_dice.h', 'licensee_host.h'}
 
 
 def test_words64():
