@@ -213,8 +213,15 @@ def main():
         for lf in prepped:
             lf.content_normalized()
         corpus.intern_files(prepped)
-        extras['host_prep_files_per_s'] = len(sample) / (time.perf_counter() - t_h)
-        extras['host_prep_note'] = 'Python normalize+intern, 1 thread, 200 synthetic texts (SURVEY 8f row 1: C++ next)'
+        extras['host_prep_python_files_per_s'] = len(sample) / (time.perf_counter() - t_h)
+        from licensee_amd.native_host import HostPrep
+        hp = HostPrep(corpus)
+        big = [synth.text(i)[0] for i in range(2000)]
+        t_h = time.perf_counter()
+        hp.prep_files(big, None, nthreads=nthreads)
+        extras['host_prep_native_files_per_s'] = len(big) / (time.perf_counter() - t_h)
+        extras['host_prep_note'] = (f'normalize+intern+Copyright/Exact of synthetic texts: Python 1 thread; '
+                                    f'native (csrc/normalize.cpp) {nthreads} threads')
 
     cpu_baseline = None
     parity = None
