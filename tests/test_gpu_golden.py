@@ -178,3 +178,27 @@ def test_dense_kernel_600_templates():
     assert np.array_equal(tks[:, 0], score)
     assert np.array_equal(np.where(tks[:, 0] >= 98.0, tki[:, 0], -1), best)
     sc.close()
+
+
+def test_batch_detector_equals_per_file_chain():
+    """batch.BatchDetector (native host Copyright/Exact + GPU Dice) == LicenseFile#license,
+    #matcher and #confidence per file (license_file.rb:92-98, project_file.rb:69-80)."""
+    from licensee_amd.batch import BatchDetector
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    texts = [c['normalized'] for t in golden('vendored.json')['templates'] for c in t['cases'].values()]
+    texts += [l.content_normalized() for l in License.all(hidden=True, pseudo=False)]
+    texts += ['Copyright (c) 2020 Foo Bar', 'Attribution-NonCommercial 4.0\n' +
+              License.find('cc-by-4.0').content_normalized(), 'café licence', '', 'not a license']
+    sc = SyntheticCorpus(TemplateCorpus(License.all(hidden=True, pseudo=False)))
+    texts += [sc.text(i, seed=7)[0] for i in range(200)]
+    det = BatchDetector(nthreads=4).detect(texts, ['LICENSE'] * len(texts))
+    kinds = set()
+    for i, t in enumerate(texts):
+        lf = LicenseFile(t, 'LICENSE')
+        m = lf.matcher()
+        assert det[i].license.key == lf.license().key, i
+        assert det[i].matcher == (m.name if m is not None else None), i
+        assert det[i].confidence == lf.confidence() and type(det[i].confidence) is type(lf.confidence()), i
+        kinds.add(det[i].matcher)
+    assert kinds == {'copyright', 'exact', 'dice', None}
