@@ -173,7 +173,7 @@ def main():
         if distributed:
             # RCCL alternative: all_gather the 16-B/file results over xGMI
             res = torch.empty((n_per, 4), dtype=torch.int32, device='cuda')
-            hip = ctypes.CDLL('libamdhip64.so')
+            hip = ctypes.CDLL('libamdhip64.so.7')   # by soname: the runtime torch already loaded
             pb, po, ps = batch.result_ptrs()
             hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
             tmp_b = torch.empty(n_per, dtype=torch.int32, device='cuda')

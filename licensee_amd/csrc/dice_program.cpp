@@ -66,6 +66,17 @@ __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { return a > b ? a - b : b 
 #define ACCM(acc, x, MASK) acc = __builtin_popcount((x) & (MASK)) + acc
 #define ACCF1(acc, x) acc = __builtin_popcount(x) + acc
 #endif
+// File-tile quad load; FILE_NT streams it with the non-temporal cache policy (each quad is
+// read exactly once per launch).
+#if FILE_NT
+typedef u32 u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldq(const uint4* p) {
+    const u32x4v v = __builtin_nontemporal_load((const u32x4v*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+#else
+__device__ __forceinline__ uint4 ldq(const uint4* p) { return *p; }
+#endif
 // Denominator (content_helper.rb:130-132,337-347); lengths are non-negative (len_F < 2^31).
 __device__ __forceinline__ i32 dn(i32 base, i32 slack, i32 tlen, u32 wf, i32 lf) {
     const i32 d = (i32)absdiff((u32)tlen, (u32)lf);
@@ -313,6 +324,8 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     for (int32_t i = 0; i < t->n_templates; ++i) max_lf = std::max(max_lf, t->lf_size[i]);
     const char* acc_asm = getenv("DICE_PROG_ACC_ASM");
     s << "#define ACC_ASM " << ((acc_asm && *acc_asm == '0') ? 0 : 1) << "\n";
+    const char* nt = getenv("DICE_PROG_NT");
+    s << "#define FILE_NT " << ((nt && *nt == '1') ? 1 : 0) << "\n";
     s << "#define WQ " << wq << "\n#define NT " << t->n_templates << "\n#define CORPUS_FAST "
       << (corpus_fast ? 1 : 0) << "\n#define NARROW_MUL " << (max_lf < (1u << 11) ? 1 : 0) << "\n" << kPrelude;
 
@@ -360,7 +373,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         const char* pd_env = getenv("DICE_PROG_PREFETCH");
         int pd = pd_env && *pd_env ? atoi(pd_env) : 8;
         pd = std::max(1, std::min<int>(pd, (int)quads.size()));
-        for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = fp[" << quads[i] * 64 << "];\n";
+        for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
         prologue << "__builtin_amdgcn_sched_barrier(0);\n";
         size_t e = 0;
         for (size_t qi = 0; qi < quads.size(); ++qi) {
@@ -368,7 +381,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             const int slot = (int)(qi % pd);
             prologue << "{ const uint4 v = pf" << slot << ";";
             if (qi + pd < quads.size())
-                prologue << " pf" << slot << " = fp[" << quads[qi + pd] * 64 << "]; __builtin_amdgcn_sched_barrier(0);";
+                prologue << " pf" << slot << " = ldq(fp + " << quads[qi + pd] * 64 << "); __builtin_amdgcn_sched_barrier(0);";
             prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
             for (; e < dm.size() && dm[e].dword / 4 == q; ++e) prologue << acc_stmt(dm[e]);
             prologue << "}\n";
@@ -379,7 +392,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             const size_t nq = quads.size();
             const size_t nqp = ((nq + pd - 1) / pd) * pd;
             std::ostringstream pp, ps;
-            for (int i = 0; i < pd; ++i) pp << "uint4 pf" << i << " = fp[" << quads[i] * 64 << "];\n";
+            for (int i = 0; i < pd; ++i) pp << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
             ps << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = 0;\n";
             size_t e2 = 0;
             for (size_t qi = 0; qi < nqp; ++qi) {
@@ -387,8 +400,8 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
                 const size_t tgt = qi + pd;
                 ps << "{ ";
                 if (qi < nq) ps << "const uint4 v = pf" << slot << "; ";
-                if (tgt < nq) ps << "pf" << slot << " = fp[" << quads[tgt] * 64 << "]; ";
-                else if (tgt >= nqp) ps << "if (has_next) pf" << slot << " = np[" << quads[tgt - nqp] * 64 << "]; ";
+                if (tgt < nq) ps << "pf" << slot << " = ldq(fp + " << quads[tgt] * 64 << "); ";
+                else if (tgt >= nqp) ps << "if (has_next) pf" << slot << " = ldq(np + " << quads[tgt - nqp] * 64 << "); ";
                 ps << "__builtin_amdgcn_sched_barrier(0);";
                 if (qi < nq) {
                     ps << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";

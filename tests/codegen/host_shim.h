@@ -8,6 +8,7 @@
 #define __launch_bounds__(...)
 #define __restrict__ __restrict
 struct uint4 { unsigned x, y, z, w; };
+static inline uint4 make_uint4(unsigned x, unsigned y, unsigned z, unsigned w) { return {x, y, z, w}; }
 struct Dim3 { unsigned x; };
 static Dim3 threadIdx, blockIdx;
 static inline bool __all(bool v) { return v; }
