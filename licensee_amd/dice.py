@@ -6,6 +6,7 @@ scores goes through the HIP library (``_native.Scorer``); there is no CPU path.
 
     Dice#matches_by_similarity       lib/licensee/matchers/dice.rb:34-41
     Dice#match / #confidence         dice.rb:8-14,51-53 (batch form: ``match_files``)
+    detect's licenses_by_similarity  commands/detect.rb:55-64,93-98 (``closest_files``)
     License#similarity(file)         content_helper.rb:128-133 (``pair_similarity``)
 """
 from __future__ import annotations
@@ -40,6 +41,19 @@ class DiceEngine:
         pairs.sort(key=lambda p: p[1])   # stable ascending, then reverse (dice.rb:39):
         pairs.reverse()                  # later key first among exact ties
         return pairs
+
+    def licenses_by_similarity(self, f) -> List[Tuple[License, float]]:
+        """The CLI's ranking (commands/detect.rb:93-98): every template, no CC filter."""
+        return self.matches_by_similarity(f, self.templates)
+
+    def closest_files(self, files: Sequence, k: int = 3) -> List[List[Tuple[License, float]]]:
+        """Batched ``licenses_by_similarity(f)[0...k]`` (detect.rb:55-64, "Closest non-matching
+        licenses") from the matrix kernel's top-k with the CC filter off."""
+        fb = self.intern(files)
+        fb.cc_false_positive[:] = 0
+        _, _, idx, score = self.scorer.matrix(fb, k)
+        return [[(self.templates[t], s) for t, s in zip(ri.tolist(), rs.tolist()) if t >= 0]
+                for ri, rs in zip(idx, score)]
 
     def match_files(self, files: Sequence, threshold=None):
         """Batched ``Dice#match``/``#confidence``: list of (License or None, confidence)."""

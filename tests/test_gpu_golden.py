@@ -202,3 +202,25 @@ def test_batch_detector_equals_per_file_chain():
         assert det[i].confidence == lf.confidence() and type(det[i].confidence) is type(lf.confidence()), i
         kinds.add(det[i].matcher)
     assert kinds == {'copyright', 'exact', 'dice', None}
+
+
+def test_closest_licenses_unfiltered_topk():
+    """detect.rb:93-98 ranks every template with no CC filter; the batched top-3 equals the
+    oracle's stable-sort-reverse ranking over all 47 templates (oracle/dice_oracle.py)."""
+    from licensee_amd.dice import default_engine
+    from oracle import dice_oracle as O
+    from tests.helpers import make_files, oracle_templates
+    eng = default_engine()
+    templates = eng.templates
+    otpl = oracle_templates(templates)
+    files = make_files(templates, 150, 33, cc_rate=0.3)
+    files += [GoldenLicenseFile(golden('dice_spec.json')['cases'][c]['file']) for c in ('cc_nd', 'gpl', 'cc_by')]
+    got = eng.closest_files(files, 3)
+    for i, f in enumerate(files):
+        of = f.oracle if hasattr(f, 'oracle') else O.OracleFile(f.content_normalized())
+        ranked = O.matches_by_similarity(otpl, of, cc_fp=False)[:3]
+        assert [(l.key, s) for l, s in got[i]] == [(templates[t].key, s) for t, s in ranked], i
+        row = eng.licenses_by_similarity(f)[:3]
+        assert [(l.key, s) for l, s in row] == [(l.key, s) for l, s in got[i]], i
+    # the cc_nd golden file is CC-flagged: Dice drops cc-* templates, the CLI ranking keeps them
+    assert any(l.key.startswith('cc-') for l, _ in got[-3])
