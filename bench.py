@@ -67,6 +67,12 @@ def main():
     ap.add_argument('--probe', action='store_true', help='diagnostic: stream-read the tiles only (read ceiling)')
     args = ap.parse_args()
 
+    # stdout carries exactly one JSON line: anything native libraries print there (RCCL's
+    # version banner at communicator init, for one) is sent to stderr instead.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -264,7 +270,7 @@ def main():
 
     if rank == 0:
         workload = {2: 'config2: synthetic perturbed LICENSE files x 47 choosealicense.com templates, Dice#match thr 98',
-                    3: 'config3: synthetic files x ~600 synthetic templates (dense kernel)',
+                    3: 'config3: synthetic files x ~600 synthetic templates (LDS-tiled sparse kernel)',
                     4: 'config4: long/mixed COPYING files (2-6 templates + notices) x 47 templates',
                     5: f'config5: full N x T similarity matrix + top-{args.topk} x 47 templates'}[cfg]
         line = {
@@ -273,7 +279,7 @@ def main():
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
             'data': 'synthetic (normalized-space perturbations of the vendored templates, seed 20250202)',
             'config': {'workload': workload, 'files_per_gpu': n_per, 'global_files': total_files,
-                       'templates': T, 'vocab': V, 'kernel': ['dense', 'sparse-program'][kind],
+                       'templates': T, 'vocab': V, 'kernel': ['dense', 'sparse-program', 'lds-sparse'][kind],
                        'program_entries': entries, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
@@ -284,7 +290,8 @@ def main():
             'parity': parity,
             'extras': extras,
         }
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + '\n').encode())
     if distributed:
         dist.destroy_process_group()
 

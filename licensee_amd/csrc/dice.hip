@@ -313,6 +313,9 @@ static void ctx_free(dice_ctx* c) {
     if (c->scratch) dice_batch_destroy(c->scratch);
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
+    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt};
+    for (void* p : plan)
+        if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -370,6 +373,12 @@ int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
     }
     // Sparse-program kernel for small corpora (see dice_program.h).
     rc = dice::program_setup(c, t);  // selects kind 1 when T <= kProgramMaxTemplates
+    if (rc == DICE_OK && c->kind == 0 && c->T > kProgramMaxTemplates) {
+        // LDS-tiled sparse kernel for large corpora (dice_lds.hip); DICE_FORCE_DENSE=1 keeps
+        // the dense kernel (A/B and tests).
+        const char* force = getenv("DICE_FORCE_DENSE");
+        if (!(force && *force == '1')) rc = dice::lds_setup(c, t);
+    }
     if (rc != DICE_OK) {
         ctx_free(c);
         return rc;
@@ -389,7 +398,7 @@ int dice_ctx_info(const dice_ctx* ctx, int32_t* T, int32_t* V, int32_t* kind, in
     if (T) *T = ctx->T;
     if (V) *V = ctx->V;
     if (kind) *kind = ctx->kind;
-    if (entries) *entries = (int32_t)ctx->prog.entries();
+    if (entries) *entries = ctx->kind == 2 ? (int32_t)ctx->lds_entries : (int32_t)ctx->prog.entries();
     return DICE_OK;
 }
 
@@ -470,6 +479,9 @@ int dice_batch_match(dice_batch* b, double thr, void* stream) {
     const unsigned grid = (unsigned)((n_tiles + (kBlock / kWave) - 1) / (kBlock / kWave));
     if (c->kind == 1) {
         int rc = dice::program_launch_match(c, b, thr, s);
+        if (rc != DICE_OK) return rc;
+    } else if (c->kind == 2) {
+        int rc = dice::lds_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,

@@ -21,6 +21,14 @@ inline int fail(int code, const std::string& msg) {
     return code;
 }
 
+inline int dalloc_bytes(void** p, size_t bytes) {
+    if (hipMalloc(p, bytes ? bytes : 1) != hipSuccess) {
+        *p = nullptr;
+        return fail(DICE_E_NOMEM, "hipMalloc failed");
+    }
+    return DICE_OK;
+}
+
 }  // namespace dice
 
 struct dice_ctx {
@@ -29,7 +37,7 @@ struct dice_ctx {
     hipStream_t stream = nullptr;
     uint4* d_tq = nullptr;  // [wq][tpad] template quads (dense kernel)
     int4* d_tc = nullptr;   // [tpad] TplConst (dense kernel)
-    int32_t kind = 0;       // 0 dense, 1 sparse program
+    int32_t kind = 0;       // 0 dense, 1 sparse program, 2 LDS-tiled sparse (T > 64)
     dice::Program prog;     // sparse program (kind 1)
     hipModule_t module = nullptr;
     hipFunction_t prog_match = nullptr;
@@ -39,7 +47,19 @@ struct dice_ctx {
     hipFunction_t prog_matrix = nullptr;    // top-k <= 4
     hipFunction_t prog_matrix16 = nullptr;  // top-k <= 16
     dice_batch* scratch = nullptr;  // reused by the host-buffer calls
+    // kind 2 plan (dice_lds.hip): per-(slab, template) entry runs, entries, wave split
+    void* d_lrec = nullptr;
+    void* d_lep = nullptr;
+    void* d_les = nullptr;
+    void* d_lwt = nullptr;
+    int32_t lds_nslab = 0, lds_npass = 0, lds_variant = 0;
+    int64_t lds_entries = 0;
 };
+
+namespace dice {
+int lds_setup(dice_ctx* c, const dice_templates* t);
+int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+}  // namespace dice
 
 struct dice_batch {
     dice_ctx* ctx = nullptr;

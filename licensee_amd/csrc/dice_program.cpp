@@ -60,6 +60,13 @@ __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { return a > b ? a - b : b 
 // acc += popcount(x & MASK): v_and_b32 (literal) + v_bcnt_u32_b32 accumulate. Written as asm
 // (ACC_ASM) because the compiler otherwise rebalances the chains into v_bcnt(x, 0) + v_add3.
 #if defined(__HIP_DEVICE_COMPILE__) && ACC_ASM
+#define ACC_ASM_ONLY(...) __VA_ARGS__
+#define ACC_C_ONLY(...)
+#else
+#define ACC_ASM_ONLY(...)
+#define ACC_C_ONLY(...) __VA_ARGS__
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && ACC_ASM
 #define ACCM(acc, x, MASK) { u32 t_; asm("v_and_b32 %1, " #MASK ", %2\n\tv_bcnt_u32_b32 %0, %1, %0" : "+v"(acc), "=&v"(t_) : "v"(x)); }
 #define ACCF1(acc, x) asm("v_bcnt_u32_b32 %0, %1, %0" : "+v"(acc) : "v"(x))
 #else
@@ -286,7 +293,7 @@ static void build_entries(const dice_templates* t, int32_t w64, Program& p) {
     }
 }
 
-// One dword-major accumulation statement.
+// One dword-major accumulation statement (plain C; ACC_C_ONLY of acc_block).
 static std::string acc_stmt(const Entry& en) {
     std::ostringstream o;
     if (en.mask == 0xFFFFFFFFu)
@@ -295,6 +302,74 @@ static std::string acc_stmt(const Entry& en) {
         o << "ACCM(acc[" << en.tpl << "], f[" << en.dword % 4 << "], 0x" << std::hex << en.mask << std::dec << ");\n";
     return o.str();
 }
+
+// A block of dword-major accumulations (entries of one quad) as ONE asm statement: the hazard
+// recognizer pads every inline-asm boundary with an s_nop, so per-entry asm would cost an
+// s_nop per v_and/v_bcnt pair. ACC_C_ONLY carries the plain-C form (host tests, ACC_ASM=0).
+static std::string acc_block(const std::vector<Entry>& dm, size_t b, size_t e) {
+    std::vector<int32_t> tpls;
+    std::vector<int> fk;
+    for (size_t i = b; i < e; ++i) {
+        if (std::find(tpls.begin(), tpls.end(), dm[i].tpl) == tpls.end()) tpls.push_back(dm[i].tpl);
+        const int k = dm[i].dword % 4;
+        if (std::find(fk.begin(), fk.end(), k) == fk.end()) fk.push_back(k);
+    }
+    auto acc_op = [&](int32_t tpl) { return (int)(std::find(tpls.begin(), tpls.end(), tpl) - tpls.begin()); };
+    // 4 temporaries: the v_and of up to 4 entries issue back to back, then their v_bcnt, so
+    // no v_bcnt waits on the v_and right before it
+    constexpr int kTmp = 4;
+    const int tmp0 = (int)tpls.size();
+    auto f_op = [&](int k) { return tmp0 + kTmp + (int)(std::find(fk.begin(), fk.end(), k) - fk.begin()); };
+    std::ostringstream a, c;
+    a << "ACC_ASM_ONLY(asm(\"";
+    bool first = true;
+    auto emit = [&](const std::string& ins) {
+        if (!first) a << "\\n\\t";
+        a << ins;
+        first = false;
+    };
+    for (size_t g = b; g < e; g += kTmp) {
+        const size_t ge = std::min(e, g + kTmp);
+        for (size_t i = g; i < ge; ++i) {
+            const Entry& en = dm[i];
+            if (en.mask == 0xFFFFFFFFu) continue;
+            std::ostringstream ins;
+            ins << "v_and_b32 %" << tmp0 + (int)(i - g) << ", 0x" << std::hex << en.mask << std::dec << ", %"
+                << f_op(en.dword % 4);
+            emit(ins.str());
+        }
+        for (size_t i = g; i < ge; ++i) {
+            const Entry& en = dm[i];
+            std::ostringstream ins;
+            const int src = en.mask == 0xFFFFFFFFu ? f_op(en.dword % 4) : tmp0 + (int)(i - g);
+            ins << "v_bcnt_u32_b32 %" << acc_op(en.tpl) << ", %" << src << ", %" << acc_op(en.tpl);
+            emit(ins.str());
+        }
+        for (size_t i = g; i < ge; ++i) c << acc_stmt(dm[i]);
+    }
+    a << "\" : ";
+    for (size_t i = 0; i < tpls.size(); ++i) a << "\"+v\"(acc[" << tpls[i] << "]), ";
+    for (int k = 0; k < kTmp; ++k) a << "\"=&v\"(t_[" << k << "])" << (k + 1 < kTmp ? ", " : "");
+    a << " : ";
+    for (size_t i = 0; i < fk.size(); ++i) a << (i ? ", " : "") << "\"v\"(f[" << fk[i] << "])";
+    a << ");)";
+    std::string cs = c.str();
+    std::replace(cs.begin(), cs.end(), '\n', ' ');
+    return "{ u32 t_[4]; " + a.str() + " ACC_C_ONLY(" + cs + ") (void)t_; }\n";
+}
+
+// Accumulations of one quad, in blocks of at most kAccBlock entries.
+static std::string acc_quad(const std::vector<Entry>& dm, size_t& e, int32_t q) {
+    const char* be = getenv("DICE_PROG_ACC_BLOCK");   // entries per asm block (A/B runs)
+    const size_t kAccBlock = be && *be ? (size_t)std::max(1, std::min(16, atoi(be))) : 8;
+    size_t end = e;
+    while (end < dm.size() && dm[end].dword / 4 == q) ++end;
+    std::string out;
+    for (size_t b = e; b < end; b += kAccBlock) out += acc_block(dm, b, std::min(end, b + kAccBlock));
+    e = end;
+    return out;
+}
+
 
 // Emits `text` as the body of a one-line-per-statement macro.
 static void emit_macro(std::ostringstream& s, const std::string& head, const std::string& text) {
@@ -383,7 +458,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             if (qi + pd < quads.size())
                 prologue << " pf" << slot << " = ldq(fp + " << quads[qi + pd] * 64 << "); __builtin_amdgcn_sched_barrier(0);";
             prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-            for (; e < dm.size() && dm[e].dword / 4 == q; ++e) prologue << acc_stmt(dm[e]);
+            prologue << acc_quad(dm, e, q);
             prologue << "}\n";
         }
         // persistent form: quad positions padded to a multiple of pd so ring slots line up
@@ -405,7 +480,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
                 ps << "__builtin_amdgcn_sched_barrier(0);";
                 if (qi < nq) {
                     ps << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                    for (; e2 < dm.size() && dm[e2].dword / 4 == quads[qi]; ++e2) ps << acc_stmt(dm[e2]);
+                    ps << acc_quad(dm, e2, quads[qi]);
                 }
                 ps << "}\n";
             }

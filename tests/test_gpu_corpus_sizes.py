@@ -1,6 +1,6 @@
 """GPU parity across corpus shapes: template counts either side of the sparse-program limit
-(64) and of the dense kernel's 48-template tile, tiny vocabularies (one 128-bit quad),
-both kernels where both apply. Bit-exact against the C oracle (oracle/dice_ref.c) for
+(64), of the dense kernel's 48-template tile and of the LDS kernel's one-pass capacity (640),
+tiny vocabularies (one 128-bit quad), every kernel where it applies. Bit-exact against the C oracle (oracle/dice_ref.c) for
 match (keys, overlaps, scores with ==) and the full similarity matrix + top-k.
 """
 import numpy as np
@@ -8,7 +8,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [1, 2, 5, 33, 47, 48, 49, 63, 64, 65, 96, 97, 130]
+SIZES = [1, 2, 5, 33, 47, 48, 49, 63, 64, 65, 96, 97, 130, 700]
 
 
 def corpus_of(n):
@@ -24,7 +24,10 @@ def corpus_of(n):
     return synthetic_templates(real, n, seed=n)
 
 
-@pytest.mark.parametrize('kernel', ['program', 'dense'])
+KIND = {'dense': 0, 'program': 1, 'lds': 2}
+
+
+@pytest.mark.parametrize('kernel', ['program', 'lds', 'dense'])
 @pytest.mark.parametrize('n_templates', SIZES)
 def test_corpus_size(n_templates, kernel, monkeypatch):
     from licensee_amd._native import Scorer
@@ -33,6 +36,8 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
     from oracle.native import OracleScorer
     if kernel == 'program' and n_templates > 64:
         pytest.skip('sparse program covers T <= 64')
+    if kernel == 'lds' and n_templates <= 64:
+        pytest.skip('LDS-tiled kernel serves T > 64')
     if kernel == 'dense':
         monkeypatch.setenv('DICE_FORCE_DENSE', '1')
     else:
@@ -41,7 +46,7 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
     fb = SyntheticCorpus(c).generate(0, 2000, seed=n_templates, nthreads=8)
     sc = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab, device=0)
     try:
-        assert sc.info()[2] == (1 if kernel == 'program' else 0)
+        assert sc.info()[2] == KIND[kernel]
         orc = OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
         for thr in (0.0, 98.0):
             best, ov, score = sc.match(fb, thr)

@@ -7,7 +7,7 @@
   * 1,000,000 synthetic files (BASELINE config 2 size): bit-exact vs the C oracle on a
     sample, plus size-independent properties over all files (idempotence, match/top-k
     consistency, top-k sortedness, CC filter).
-  * Dense kernel at T = 600 synthetic templates (config 3 regime) vs the C oracle.
+  * LDS-tiled and dense kernels at T = 600 synthetic templates (config 3 regime) vs the C oracle.
 """
 import json
 import os
@@ -155,7 +155,8 @@ def test_full_size_matrix_consistency(big):
     assert not np.isin(tki[flagged], cc_t).any()
 
 
-def test_dense_kernel_600_templates():
+@pytest.mark.parametrize('kernel', ['lds', 'dense'])
+def test_large_corpus_600_templates(kernel, monkeypatch):
     from licensee_amd._native import Scorer
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
@@ -164,9 +165,13 @@ def test_dense_kernel_600_templates():
     tpl = synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=5)
     corpus = TemplateCorpus(tpl)
     fb = SyntheticCorpus(corpus).generate(0, 3000, seed=11, nthreads=8)
+    if kernel == 'dense':
+        monkeypatch.setenv('DICE_FORCE_DENSE', '1')
+    else:
+        monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
     sc = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
                 corpus.is_cc, corpus.n_vocab, device=0)
-    assert sc.info()[2] == 0   # dense kernel for T > 64
+    assert sc.info()[2] == {'lds': 2, 'dense': 0}[kernel]
     orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
                        corpus.length, corpus.is_cc, corpus.n_vocab)
     best, ov, score = sc.match(fb, 98.0)
