@@ -8,6 +8,8 @@
  *   LicenseFile#potential_false_positive?                lib/licensee/project_files/license_file.rb:80-82
  *   Matchers::Copyright#match                            lib/licensee/matchers/copyright.rb:12-17
  *   Matchers::Exact#match                                lib/licensee/matchers/exact.rb:6-12
+ * and packs the template vocabulary for the device bitsets (word ids are free: the overlap
+ * of content_helper.rb:129 counts set members, so any order gives identical scores).
  * The regular expressions are supplied by the caller (licensee_amd/content_helper.py passes
  * its compiled patterns), so host paths share one pattern source. Texts outside the native
  * envelope (non-ASCII letters, HTML) report status 1 and are prepared by the caller.
@@ -45,6 +47,16 @@ int lh_prep_files(lh_ctx *ctx, int64_t n, const char *const *data, const int64_t
                   const char *const *filenames, int32_t nthreads, uint64_t *bits, uint32_t *wf,
                   int32_t *length, uint8_t *cc, uint8_t *copyright, int32_t *exact,
                   uint8_t *status);
+
+/* Vocabulary packing (csrc/vocab_pack.cpp): local search over word swaps between bins of
+ * bin_bits (32: sparse-program (template, dword) instruction pairs; 64: LDS-kernel
+ * (template, u64) records), starting from `init` (a permutation of 0..V-1). sig is
+ * [V][sig_words] template-membership bitsets (bit t = word in template t's Lf). Writes the
+ * new order (position -> word id of `sig`) to out; returns its cost, or -1 on bad input.
+ * Deterministic for a given seed. */
+int64_t lh_vocab_pack(const uint64_t *sig, int32_t n_vocab, int32_t sig_words, int32_t n_templates,
+                      const int32_t *init, int32_t bin_bits, int64_t iters, uint64_t seed,
+                      int32_t *out);
 
 #ifdef __cplusplus
 }

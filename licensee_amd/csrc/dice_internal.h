@@ -41,9 +41,6 @@ struct dice_ctx {
     dice::Program prog;     // sparse program (kind 1)
     hipModule_t module = nullptr;
     hipFunction_t prog_match = nullptr;
-    hipFunction_t prog_match_p = nullptr;   // persistent match variant (DICE_PROG_PERSIST=1)
-    int64_t persist_waves = 0;              // resident wave capacity for prog_match_p
-    bool use_persist = false;
     hipFunction_t prog_matrix = nullptr;    // top-k <= 4
     hipFunction_t prog_matrix16 = nullptr;  // top-k <= 16
     dice_batch* scratch = nullptr;  // reused by the host-buffer calls

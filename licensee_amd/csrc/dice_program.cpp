@@ -75,7 +75,7 @@ __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { return a > b ? a - b : b 
 #endif
 // File-tile quad load; FILE_NT streams it with the non-temporal cache policy (each quad is
 // read exactly once per launch).
-#if FILE_NT
+#if FILE_NT && defined(__HIP_DEVICE_COMPILE__)
 typedef u32 u32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ldq(const uint4* p) {
     const u32x4v v = __builtin_nontemporal_load((const u32x4v*)p);
@@ -133,49 +133,6 @@ extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
         best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
         ov_out[file] = bo;
         score_out[file] = s;
-    }
-}
-)HIP";
-
-// Persistent match kernel: grid = resident capacity; each wave walks tiles tile, tile+stride...
-// and its quad prefetch ring keeps streaming across tile boundaries (PERSIST_BODY).
-const char* kMatchPersistKernel = R"HIP(
-extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match_p(
-    const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
-    const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
-    u32* __restrict__ ov_out, double* __restrict__ score_out) {
-    const int lane = threadIdx.x & 63;
-    const i64 ntiles = (n + 63) / 64;
-    const i64 stride = (i64)gridDim.x * 4;
-    i64 tile = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= ntiles) return;
-    const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
-    PERSIST_PROLOGUE
-    for (;;) {
-        const i64 file = tile * 64 + lane;
-        const i64 next = tile + stride;
-        const bool has_next = next < ntiles;
-        const uint4* np = files + next * (i64)(WQ * 64) + lane;
-        const u32 wf = wfp[file];
-        const i32 lf = lenp[file];
-        const bool cc = ccp[file] != 0;
-        const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
-        PERSIST_STREAM
-        i32 bi = -1; u32 bo = 0; i32 bd = 1;
-        if (__all(fast)) {
-            MATCH_BODY(true)
-        } else {
-            MATCH_BODY(false)
-        }
-        if (file < n) {
-            const double s = bi >= 0 ? sc(bo, bd) : 0.0;
-            best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
-            ov_out[file] = bo;
-            score_out[file] = s;
-        }
-        if (!has_next) break;
-        tile = next;
-        fp = np;
     }
 }
 )HIP";
@@ -365,6 +322,12 @@ static std::string acc_quad(const std::vector<Entry>& dm, size_t& e, int32_t q) 
     size_t end = e;
     while (end < dm.size() && dm[end].dword / 4 == q) ++end;
     std::string out;
+    const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
+    if (diag && strcmp(diag, "noacc") == 0) {
+        out = "acc[" + std::to_string(q) + " % NT] ^= f[0] ^ f[1] ^ f[2] ^ f[3];\n";
+        e = end;
+        return out;
+    }
     for (size_t b = e; b < end; b += kAccBlock) out += acc_block(dm, b, std::min(end, b + kAccBlock));
     e = end;
     return out;
@@ -400,7 +363,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     const char* acc_asm = getenv("DICE_PROG_ACC_ASM");
     s << "#define ACC_ASM " << ((acc_asm && *acc_asm == '0') ? 0 : 1) << "\n";
     const char* nt = getenv("DICE_PROG_NT");
-    s << "#define FILE_NT " << ((nt && *nt == '1') ? 1 : 0) << "\n";
+    s << "#define FILE_NT " << ((nt && *nt == '0') ? 0 : 1) << "\n";
     s << "#define WQ " << wq << "\n#define NT " << t->n_templates << "\n#define CORPUS_FAST "
       << (corpus_fast ? 1 : 0) << "\n#define NARROW_MUL " << (max_lf < (1u << 11) ? 1 : 0) << "\n" << kPrelude;
 
@@ -440,52 +403,62 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             return x.dword != y.dword ? x.dword < y.dword : x.tpl < y.tpl;
         });
         prologue << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = 0;\n";
-        // quads the program touches, in order; a ring of `pd` registers prefetches quad i+pd
-        // while quad i is consumed; sched_barrier pins each load where it is issued.
+        // quads the program touches, in order
         std::vector<int32_t> quads;
         for (const Entry& en : dm)
             if (quads.empty() || quads.back() != en.dword / 4) quads.push_back(en.dword / 4);
-        const char* pd_env = getenv("DICE_PROG_PREFETCH");
-        int pd = pd_env && *pd_env ? atoi(pd_env) : 8;
-        pd = std::max(1, std::min<int>(pd, (int)quads.size()));
-        for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
-        prologue << "__builtin_amdgcn_sched_barrier(0);\n";
-        size_t e = 0;
-        for (size_t qi = 0; qi < quads.size(); ++qi) {
-            const int32_t q = quads[qi];
-            const int slot = (int)(qi % pd);
-            prologue << "{ const uint4 v = pf" << slot << ";";
-            if (qi + pd < quads.size())
-                prologue << " pf" << slot << " = ldq(fp + " << quads[qi + pd] * 64 << "); __builtin_amdgcn_sched_barrier(0);";
-            prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-            prologue << acc_quad(dm, e, q);
-            prologue << "}\n";
-        }
-        // persistent form: quad positions padded to a multiple of pd so ring slots line up
-        // across tiles; positions >= nq only prefetch the next tile.
-        {
-            const size_t nq = quads.size();
-            const size_t nqp = ((nq + pd - 1) / pd) * pd;
-            std::ostringstream pp, ps;
-            for (int i = 0; i < pd; ++i) pp << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
-            ps << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = 0;\n";
-            size_t e2 = 0;
-            for (size_t qi = 0; qi < nqp; ++qi) {
+        const char* sched_env = getenv("DICE_PROG_SCHED");
+        const bool ring = sched_env && strcmp(sched_env, "ring") == 0;
+        if (ring) {
+            // ring of `pd` registers: quad i+pd is requested as quad i is consumed
+            const char* pd_env = getenv("DICE_PROG_PREFETCH");
+            int pd = pd_env && *pd_env ? atoi(pd_env) : 8;
+            pd = std::max(1, std::min<int>(pd, (int)quads.size()));
+            for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
+            prologue << "__builtin_amdgcn_sched_barrier(0);\n";
+            size_t e = 0;
+            for (size_t qi = 0; qi < quads.size(); ++qi) {
                 const int slot = (int)(qi % pd);
-                const size_t tgt = qi + pd;
-                ps << "{ ";
-                if (qi < nq) ps << "const uint4 v = pf" << slot << "; ";
-                if (tgt < nq) ps << "pf" << slot << " = ldq(fp + " << quads[tgt] * 64 << "); ";
-                else if (tgt >= nqp) ps << "if (has_next) pf" << slot << " = ldq(np + " << quads[tgt - nqp] * 64 << "); ";
-                ps << "__builtin_amdgcn_sched_barrier(0);";
-                if (qi < nq) {
-                    ps << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                    ps << acc_quad(dm, e2, quads[qi]);
-                }
-                ps << "}\n";
+                prologue << "{ const uint4 v = pf" << slot << ";";
+                if (qi + pd < quads.size())
+                    prologue << " pf" << slot << " = ldq(fp + " << quads[qi + pd] * 64 << "); __builtin_amdgcn_sched_barrier(0);";
+                prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
+                prologue << acc_quad(dm, e, quads[qi]);
+                prologue << "}\n";
             }
-            emit_macro(s, "PERSIST_PROLOGUE", pp.str());
-            emit_macro(s, "PERSIST_STREAM", ps.str());
+        } else {
+            // bursts (default): quads in groups of `nb`, double-buffered in register sets
+            // p0_* / p1_*; group g+1 is requested (nb contiguous 1 KiB wave loads back to back)
+            // before group g is consumed. With non-temporal loads, nb = 3 measured ~1.5% ahead
+            // of the 8-deep ring at 92 instead of 124 VGPRs (same box, interleaved A/B runs).
+            const char* b_env = getenv("DICE_PROG_BURST");
+            int nb = b_env && *b_env ? atoi(b_env) : 3;
+            nb = std::max(1, std::min<int>(nb, (int)quads.size()));
+            const size_t ng = (quads.size() + nb - 1) / nb;
+            auto group_loads = [&](std::ostringstream& o, size_t g, int set) {
+                for (size_t i = g * nb; i < std::min(quads.size(), (g + 1) * nb); ++i)
+                    o << "p" << set << "_" << (i - g * nb) << " = ldq(fp + " << quads[i] * 64 << "); ";
+                o << "\n";
+            };
+            auto stream = [&](std::ostringstream& o) {
+                size_t e = 0;
+                for (size_t g = 0; g < ng; ++g) {
+                    const int cur = (int)(g % 2), nxt = 1 - cur;
+                    o << "__builtin_amdgcn_sched_barrier(0);\n";
+                    if (g + 1 < ng) group_loads(o, g + 1, nxt);
+                    o << "__builtin_amdgcn_sched_barrier(0);\n";
+                    for (size_t i = g * nb; i < std::min(quads.size(), (g + 1) * nb); ++i) {
+                        o << "{ const uint4 v = p" << cur << "_" << (i - g * nb) << "; const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
+                        o << acc_quad(dm, e, quads[i]);
+                        o << "}\n";
+                    }
+                }
+            };
+            std::ostringstream decl;
+            for (int i = 0; i < nb; ++i) decl << "uint4 p0_" << i << ", p1_" << i << ";\n";
+            prologue << decl.str();
+            group_loads(prologue, 0, 0);
+            stream(prologue);
         }
         for (int32_t i = 0; i < t->n_templates; ++i) {
             match_body << "{ const u32 a = acc[" << i << "]; i32 d; " << den[i] << offer(i) << " }\n";
@@ -494,9 +467,14 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         }
     }
     emit_macro(s, "FILE_PROLOGUE", prologue.str());
+    const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
+    if (diag && strcmp(diag, "noepi") == 0) {
+        std::ostringstream mb;
+        mb << "bi = 0; bd = 1; bo = 0; _Pragma(\"unroll\") for (int i = 0; i < NT; ++i) bo += acc[i];\n";
+        match_body.str(mb.str());
+    }
     emit_macro(s, "MATCH_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", match_body.str() + "}");
     s << kMatchKernel;
-    if (order == 'd') s << kMatchPersistKernel;
     s << kMatrixOffer;
     emit_macro(s, "MATRIX_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", matrix_body.str() + "}");
     for (int km : {4, 16}) {
@@ -548,18 +526,6 @@ static int compile_or_load(dice_ctx* c, const std::string& src) {
     int rc = compile_cached(src, code, nullptr);
     if (rc != DICE_OK) return rc;
     if (hipModuleLoadData(&c->module, code.data()) != hipSuccess) return fail(DICE_E_DEVICE, "hipModuleLoadData failed");
-    c->prog_match_p = nullptr;
-    if (hipModuleGetFunction(&c->prog_match_p, c->module, "dice_prog_match_p") != hipSuccess) c->prog_match_p = nullptr;
-    (void)hipGetLastError();
-    if (c->prog_match_p) {
-        int nb = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, c->prog_match_p, 256, 0) != hipSuccess) nb = 0;
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) prop.multiProcessorCount = 0;
-        c->persist_waves = (int64_t)nb * prop.multiProcessorCount * 4;
-        const char* pe = getenv("DICE_PROG_PERSIST");
-        c->use_persist = pe && *pe == '1' && c->persist_waves > 0;
-    }
     if (hipModuleGetFunction(&c->prog_match, c->module, "dice_prog_match") != hipSuccess ||
         hipModuleGetFunction(&c->prog_matrix, c->module, "dice_prog_matrix4") != hipSuccess ||
         hipModuleGetFunction(&c->prog_matrix16, c->module, "dice_prog_matrix16") != hipSuccess)
@@ -602,15 +568,8 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
 
 int program_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + 63) / 64;
-    unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    const unsigned grid = (unsigned)((n_tiles + 3) / 4);
     hipFunction_t fn = c->prog_match;
-    if (c->use_persist) {
-        // as many resident waves as needed for equal tile counts per wave
-        const int64_t rounds = (n_tiles + c->persist_waves - 1) / c->persist_waves;
-        const int64_t waves = (n_tiles + rounds - 1) / rounds;
-        grid = (unsigned)((waves + 3) / 4);
-        fn = c->prog_match_p;
-    }
     int64_t n = b->n;
     void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score};
     if (hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)

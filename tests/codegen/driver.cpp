@@ -30,18 +30,6 @@ int main(int argc, char** argv) {
             (k <= 4 ? dice_prog_matrix4 : dice_prog_matrix16)(tiles.data(), n, wf.data(), len.data(), cc.data(), k, mov.data(), msc.data(),
                              k ? tki.data() : nullptr, tks.data());
         }
-#ifdef HAS_PERSIST
-    {   // persistent variant, emulating a grid of 1 block (4 waves) walking all tiles
-        std::vector<i32> best2(n); std::vector<u32> ov2(n); std::vector<double> sc2(n);
-        struct Dim3g { unsigned x; };
-        for (unsigned bk = 0; bk < 1; ++bk)
-            for (unsigned t = 0; t < 256; ++t) {
-                blockIdx.x = bk; threadIdx.x = t;
-                dice_prog_match_p(tiles.data(), n, wf.data(), len.data(), cc.data(), 98.0, best2.data(), ov2.data(), sc2.data());
-            }
-        if (best2 != best || ov2 != ov || sc2 != sc_) { fprintf(stderr, "persistent kernel mismatch\n"); return 3; }
-    }
-#endif
     snprintf(p, sizeof p, "%s/best.out", d); save(p, best);
     snprintf(p, sizeof p, "%s/ov.out", d); save(p, ov);
     snprintf(p, sizeof p, "%s/score.out", d); save(p, sc_);

@@ -31,7 +31,7 @@ def test_host_library_exports_every_declared_symbol():
     from licensee_amd import native_host
     lib = native_host._load()
     declared = declared_functions('licensee_host.h', 'lh_')
-    assert declared == {'lh_create', 'lh_destroy', 'lh_set_templates', 'lh_normalize', 'lh_prep_files'}
+    assert declared == {'lh_create', 'lh_destroy', 'lh_set_templates', 'lh_normalize', 'lh_prep_files', 'lh_vocab_pack'}
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(os.listdir(os.path.join(ROOT, 'include'))) == {'licensee_dice.h', 'licensee_host.h'}
@@ -80,3 +80,43 @@ def test_program_source_and_precompile_without_device():
     path = ctypes.create_string_buffer(1024)
     assert lib.dice_precompile(ctypes.byref(t), path, 1024) == 0
     assert os.path.exists(path.value.decode())
+
+
+def test_vocab_pack_is_a_permutation_and_never_worse():
+    """lh_vocab_pack (csrc/vocab_pack.cpp): the packed order is a permutation, its reported
+    cost is the true (template, dword) cost and never above the starting order's."""
+    import ctypes
+
+    import numpy as np
+
+    from licensee_amd import native_host
+    lib = native_host._load()
+    fn = lib.lh_vocab_pack
+    fn.restype = ctypes.c_int64
+    vp = ctypes.c_void_p
+    fn.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int64,
+                   ctypes.c_uint64, vp]
+    rng = np.random.default_rng(5)
+    for T, V, bin_bits in ((20, 700, 32), (130, 900, 64)):
+        W = (T + 63) // 64
+        M = rng.random((V, T)) < rng.random(T) * 0.3
+        M[np.arange(V), rng.integers(0, T, V)] = True       # every word in >= 1 template
+        sig = np.zeros((V, W), np.uint64)
+        for t in range(T):
+            sig[:, t // 64] |= M[:, t].astype(np.uint64) << np.uint64(t % 64)
+
+        def cost(order):
+            c = 0
+            for b in range(0, V, bin_bits):
+                ws = order[b:b + bin_bits]
+                anyt, allt = M[ws].any(0), M[ws].all(0) & (len(ws) == 32)
+                c += int(anyt.sum()) * (2 if bin_bits == 32 else 1) - (int(allt.sum()) if bin_bits == 32 else 0)
+            return c
+        init = rng.permutation(V).astype(np.int32)
+        out = np.empty(V, np.int32)
+        got = fn(sig.ctypes.data, V, W, T, init.ctypes.data, bin_bits, 200000, 7, out.ctypes.data)
+        assert sorted(out.tolist()) == list(range(V))
+        assert got == cost(out) <= cost(init)
+        bad = init.copy()
+        bad[0] = bad[1]
+        assert fn(sig.ctypes.data, V, W, T, bad.ctypes.data, bin_bits, 10, 7, out.ctypes.data) == -1

@@ -51,8 +51,7 @@ def run_host(corpus, fb, k, tmp_path):
         fh.write(src)
     shutil.copy(os.path.join(HERE, 'codegen', 'host_shim.h'), d)
     exe = os.path.join(d, 'drv')
-    defs = ['-DHAS_PERSIST'] if 'dice_prog_match_p' in src else []
-    subprocess.run(['g++', '-O1', '-std=c++17', '-w', '-I', d] + defs + ['-o', exe, os.path.join(HERE, 'codegen', 'driver.cpp')],
+    subprocess.run(['g++', '-O1', '-std=c++17', '-w', '-I', d, '-o', exe, os.path.join(HERE, 'codegen', 'driver.cpp')],
                    check=True)
     wq = (corpus.w64 + 1) // 2
     n = fb.n
@@ -72,9 +71,20 @@ def run_host(corpus, fb, k, tmp_path):
             rd('tki.out', np.int32).reshape(max(k, 1), n)[:k].T, rd('tks.out', np.float64).reshape(max(k, 1), n)[:k].T)
 
 
+SCHEDULES = {
+    'burst3': {},                                    # default: bursts of 3 quads, non-temporal loads
+    'burst7': {'DICE_PROG_BURST': '7', 'DICE_PROG_NT': '0'},
+    'ring8': {'DICE_PROG_SCHED': 'ring'},
+}
+
+
 @pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
-@pytest.mark.parametrize('k', [3, 5])
-def test_generated_program_matches_oracle(tmp_path, k):
+@pytest.mark.parametrize('k,sched', [(3, 'burst3'), (5, 'burst7'), (5, 'ring8')])
+def test_generated_program_matches_oracle(tmp_path, monkeypatch, k, sched):
+    for key in ('DICE_PROG_SCHED', 'DICE_PROG_BURST', 'DICE_PROG_NT'):
+        monkeypatch.delenv(key, raising=False)
+    for key, v in SCHEDULES[sched].items():
+        monkeypatch.setenv(key, v)
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.license import License
     from oracle import dice_oracle as O
