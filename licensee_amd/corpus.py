@@ -77,7 +77,7 @@ def pack_vocabulary(order: List[str], members: Dict[str, List[int]], n_templates
     cached in-process and under lib/cache by a hash of the signatures. Without the native
     host library the order is returned unchanged (scores do not depend on the order)."""
     V = len(order)
-    if V < 2:
+    if V < 2 or n_templates < 2:   # one template: every word has the same signature
         return order
     W = (n_templates + 63) // 64
     sig = np.zeros((V, W), np.uint64)

@@ -157,7 +157,7 @@ __device__ __forceinline__ bool outranks(int32_t ai, uint32_t ao, int32_t ad, in
     return ge && (!le || ai > bi);
 }
 
-template <int F, int G>
+template <int F, int G, bool R3>
 __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
     const uint4* __restrict__ tiles, int64_t n, int32_t wq, int32_t nslab, int32_t T,
     const int32_t* __restrict__ rec, const uint4* __restrict__ ep, const int32_t* __restrict__ wave_t0,
@@ -233,11 +233,26 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
                     uint4 c0, c1, c2, c3, d0, d1, d2, d3;
                     load4(ee, c0, c1, c2, c3);
                     int32_t e = 0;
-                    for (; e + 8 <= cnt; e += 8) {   // ping-pong: no SGPR copies
-                        step4<F>(acc[j], base, c0, c1, c2, c3, ee + e + 4, d0, d1, d2, d3);
-                        step4<F>(acc[j], base, d0, d1, d2, d3, ee + e + 8, c0, c1, c2, c3);
+                    if constexpr (R3) {
+                        // three record sets in rotation: the records of step s + 2 are
+                        // requested during step s, so a scalar load has two steps of vector
+                        // work to arrive (the table is padded 8 records past every run end)
+                        uint4 g0, g1, g2, g3;
+                        load4(ee + 4, d0, d1, d2, d3);
+                        for (; e + 12 <= cnt; e += 12) {
+                            step4<F>(acc[j], base, c0, c1, c2, c3, ee + e + 8, g0, g1, g2, g3);
+                            step4<F>(acc[j], base, d0, d1, d2, d3, ee + e + 12, c0, c1, c2, c3);
+                            step4<F>(acc[j], base, g0, g1, g2, g3, ee + e + 16, d0, d1, d2, d3);
+                        }
+                        if (e < cnt) step4<F>(acc[j], base, c0, c1, c2, c3, ee + e + 8, g0, g1, g2, g3);
+                        if (e + 4 < cnt) step4<F>(acc[j], base, d0, d1, d2, d3, ee + e + 12, c0, c1, c2, c3);
+                    } else {
+                        for (; e + 8 <= cnt; e += 8) {   // ping-pong: no SGPR copies
+                            step4<F>(acc[j], base, c0, c1, c2, c3, ee + e + 4, d0, d1, d2, d3);
+                            step4<F>(acc[j], base, d0, d1, d2, d3, ee + e + 8, c0, c1, c2, c3);
+                        }
+                        if (e < cnt) step4<F>(acc[j], base, c0, c1, c2, c3, ee + e + 4, d0, d1, d2, d3);
                     }
-                    if (e < cnt) step4<F>(acc[j], base, c0, c1, c2, c3, ee + e + 4, d0, d1, d2, d3);
                 }
             }
         }
@@ -317,14 +332,19 @@ static std::vector<int32_t> split_waves(const std::vector<int64_t>& cost, int32_
 
 struct Variant {
     int f, g;
+    bool r3;
 };
-static const Variant kVariants[] = {{4, 16}, {4, 8}, {2, 16}, {2, 24}};
+static const Variant kVariants[] = {{4, 16, false}, {4, 8, false}, {2, 16, false}, {2, 24, false},
+                                    {4, 16, true}, {4, 8, true}, {2, 24, true}};
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
 static int slab_pairs(int f) { return kLdsBytes / (f * kWave * 8); }
 
 int lds_setup(dice_ctx* c, const dice_templates* t) {
     const char* ve = getenv("DICE_LDS_VARIANT");
-    const int vi = ve && *ve ? std::max(0, std::min(3, atoi(ve))) : 0;
+    // default: 2 tiles x 24 templates per wave with the 3-set record rotation -- no scratch
+    // spills (113 VGPRs; F=4 x G=16 spills 32 B/lane) and 2 passes instead of 3 at T = 600
+    const int vi = ve && *ve ? std::max(0, std::min(kNumVariants - 1, atoi(ve))) : 6;
     const int F = kVariants[vi].f, G = kVariants[vi].g;
     const int32_t kSlabPairs = slab_pairs(F), kPairBytes = F * kWave * 8;
     const int32_t T = c->T, w64 = c->w64;
@@ -374,11 +394,11 @@ int lds_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
-template <int F, int G>
+template <int F, int G, bool R3>
 static void launch(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + kWave - 1) / kWave;
     const int64_t groups = (n_tiles + F - 1) / F;
-    hipLaunchKernelGGL((dice_lds_match<F, G>), dim3((unsigned)groups), dim3(kLdsWaves * kWave), 0, s, b->d_tiles,
+    hipLaunchKernelGGL((dice_lds_match<F, G, R3>), dim3((unsigned)groups), dim3(kLdsWaves * kWave), 0, s, b->d_tiles,
                        b->n, c->wq, c->lds_nslab, c->T, (const int32_t*)c->d_lrec, (const uint4*)c->d_lep,
                        (const int32_t*)c->d_lwt, c->lds_npass, c->d_tc, b->d_wf, b->d_len, b->d_cc, thr,
                        b->d_best, b->d_ov, b->d_score);
@@ -386,10 +406,13 @@ static void launch(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
 
 int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     switch (c->lds_variant) {
-        case 0: launch<4, 16>(c, b, thr, s); break;
-        case 1: launch<4, 8>(c, b, thr, s); break;
-        case 2: launch<2, 16>(c, b, thr, s); break;
-        default: launch<2, 24>(c, b, thr, s); break;
+        case 0: launch<4, 16, false>(c, b, thr, s); break;
+        case 1: launch<4, 8, false>(c, b, thr, s); break;
+        case 2: launch<2, 16, false>(c, b, thr, s); break;
+        case 3: launch<2, 24, false>(c, b, thr, s); break;
+        case 4: launch<4, 16, true>(c, b, thr, s); break;
+        case 5: launch<4, 8, true>(c, b, thr, s); break;
+        default: launch<2, 24, true>(c, b, thr, s); break;
     }
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_lds_match launch failed");
 }

@@ -27,17 +27,18 @@ def corpus_of(n):
 KIND = {'dense': 0, 'program': 1, 'lds': 2}
 
 
-@pytest.mark.parametrize('kernel', ['program', 'lds', 'dense'])
-@pytest.mark.parametrize('n_templates', SIZES)
+# every kernel where it applies: the sparse program serves T <= 64, the LDS kernel T > 64,
+# the dense kernel (DICE_FORCE_DENSE) any T
+CASES = [(n, k) for n in SIZES for k in ('program', 'lds', 'dense')
+         if not (k == 'program' and n > 64) and not (k == 'lds' and n <= 64)]
+
+
+@pytest.mark.parametrize('n_templates,kernel', CASES)
 def test_corpus_size(n_templates, kernel, monkeypatch):
     from licensee_amd._native import Scorer
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
     from oracle.native import OracleScorer
-    if kernel == 'program' and n_templates > 64:
-        pytest.skip('sparse program covers T <= 64')
-    if kernel == 'lds' and n_templates <= 64:
-        pytest.skip('LDS-tiled kernel serves T > 64')
     if kernel == 'dense':
         monkeypatch.setenv('DICE_FORCE_DENSE', '1')
     else:

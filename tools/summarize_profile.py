@@ -22,7 +22,7 @@ def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_stats.csv'))))
     # the product kernel of the timed region (copies/packing outside it are listed, not chosen)
-    product = [r for r in stats if r['Name'].replace('void ', '').startswith(('dice_prog_', 'dice_dense_'))]
+    product = [r for r in stats if r['Name'].replace('void ', '').startswith(('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice::dice_lds_'))]
     top = max(product or stats, key=lambda r: float(r['TotalDurationNs']))
     kernel = top['Name'].split('(')[0].replace('void ', '')
     avg_ns = float(top['AverageNs'])
