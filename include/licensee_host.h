@@ -38,6 +38,14 @@ int lh_set_templates(lh_ctx *ctx, int32_t n_templates, const uint64_t *lf_bits,
                      const uint32_t *wordset_size, const int32_t *field_off,
                      const char *const *field_words);
 
+/* Unicode tables, so texts with non-ASCII letters stay native (without them the native
+ * envelope is ASCII letters only). lower_*: every non-ASCII code point whose Python
+ * str.lower() is a different single code point; word_lo/hi: sorted inclusive ranges of the
+ * non-ASCII code points with str.isalnum() True (Python's \w for \b). The caller derives
+ * both from its own Unicode database (licensee_amd/native_host.py). 0 or -1 on bad input. */
+int lh_set_unicode(lh_ctx *ctx, int32_t n_lower, const uint32_t *lower_from, const uint32_t *lower_to,
+                   int32_t n_word, const uint32_t *word_lo, const uint32_t *word_hi);
+
 /* content_normalized of one text (UTF-8 out); -1 = outside the native envelope. */
 int64_t lh_normalize(lh_ctx *ctx, const char *data, int64_t len, const char *filename,
                      int32_t is_file, char *out, int64_t cap);

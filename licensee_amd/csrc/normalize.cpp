@@ -71,9 +71,19 @@ bool safe_nonascii(char32_t c) {
     return false;
 }
 
+// With the Unicode tables installed, the only texts left to the Python path are those with a
+// character whose Python semantics are not a per-character table lookup: the letters re.I
+// equates with ASCII ones (U+0130 İ, U+0131 ı, U+017F ſ, U+212A Kelvin K; U+0130 also lowers
+// to two characters) and U+03A3 Σ (str.lower() applies the Final_Sigma context rule).
+bool python_only(char32_t c) { return c == 0x130 || c == 0x131 || c == 0x17F || c == 0x212A || c == 0x3A3; }
+
 struct Ctx {
     std::map<std::string, Regex> re;
     std::vector<std::pair<Str, Str>> spell;
+    std::vector<int> spell_first[128];   // spell indices by first character, union order kept
+    // Unicode tables (lh_set_unicode): Python str.lower() of non-ASCII code points
+    bool unicode = false;
+    std::unordered_map<char32_t, char32_t> lower;
     std::unordered_map<std::string, int32_t> vocab;
     int32_t n_vocab = 0, w64 = 0;
     // templates (Exact)
@@ -89,9 +99,17 @@ struct Ctx {
 struct Normalizer {
     const Ctx& c;
     Str cur;
+    bool clean = false;   // cur is already squeezed and stripped (a strip op without a match is a no-op)
 
-    void strip_re(const Regex& r) { cur = ruby_strip(squeeze_spaces(r.sub(cur, U" "))); }
-    void sub_re(const Regex& r, const char32_t* repl) { cur = r.sub(cur, Str(repl)); }
+    // strip(re): gsub(re, ' ').squeeze(' ').strip (content_helper.rb:223-236)
+    void strip_re(const Regex& r) {
+        if (!r.sub_into(cur, U" ") && clean) return;
+        cur = ruby_strip(squeeze_spaces(cur));
+        clean = true;
+    }
+    void sub_re(const Regex& r, const char32_t* repl) {
+        if (r.sub_into(cur, Str(repl))) clean = false;
+    }
 
     void strip_title() {
         const Regex& t = c.R("title");
@@ -134,29 +152,37 @@ struct Normalizer {
     // alternatives, tried only where \b can hold before a letter (a word start); text on this
     // path has ASCII word characters only, so \b is the ASCII boundary.
     void spelling() {
-        Str out;
-        out.reserve(cur.size());
         const size_t n = cur.size();
-        size_t i = 0;
-        auto word = [](char32_t ch) { return (ch >= 'a' && ch <= 'z') || (ch >= 'A' && ch <= 'Z') || (ch >= '0' && ch <= '9') || ch == '_'; };
-        while (i < n) {
-            if (word(cur[i]) && (i == 0 || !word(cur[i - 1]))) {
-                bool hit = false;
-                for (auto& kv : c.spell) {
-                    const Str& k = kv.first;
-                    if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 &&
-                        (i + k.size() == n || !word(cur[i + k.size()]))) {
-                        out += kv.second;
-                        i += k.size();
-                        hit = true;
-                        break;
-                    }
+        auto word = [](char32_t ch) { return rx::is_word_char(ch); };   // Python \b's \w
+        // the replacement of the key matching at word start i, or nullptr
+        auto match_at = [&](size_t i, size_t& klen) -> const Str* {
+            if (cur[i] >= 128 || !word(cur[i]) || (i > 0 && word(cur[i - 1]))) return nullptr;
+            for (int si : c.spell_first[cur[i]]) {
+                const Str& k = c.spell[si].first;
+                if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 && (i + k.size() == n || !word(cur[i + k.size()]))) {
+                    klen = k.size();
+                    return &c.spell[si].second;
                 }
-                if (hit) continue;
             }
-            out.push_back(cur[i++]);
+            return nullptr;
+        };
+        size_t i = 0, klen = 0;
+        const Str* rep = nullptr;
+        while (i < n && !(rep = match_at(i, klen))) ++i;
+        if (!rep) return;   // no varietal word: nothing to rebuild
+        Str out(cur, 0, i);
+        out.reserve(n);
+        while (i < n) {
+            if (rep) {
+                out += *rep;
+                i += klen;
+            } else {
+                out.push_back(cur[i++]);
+            }
+            rep = i < n ? match_at(i, klen) : nullptr;
         }
         cur.swap(out);
+        clean = false;
     }
 
     // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip
@@ -169,6 +195,7 @@ struct Normalizer {
             else out.push_back(ch);
         }
         cur = ruby_strip(out);
+        clean = true;
     }
 
     // content_without_title_and_version + content_normalized (content_helper.rb:144-168)
@@ -180,8 +207,14 @@ struct Normalizer {
         sub_re(c.R("link_markup"), U"\\1");
         strip_title();
         strip_re(c.R("version"));
-        for (auto& ch : cur)
-            if (ch >= 'A' && ch <= 'Z') ch += 32;
+        for (auto& ch : cur) {
+            if (ch < 128) {
+                if (ch >= 'A' && ch <= 'Z') ch += 32;
+            } else if (c.unicode) {
+                auto it = c.lower.find(ch);
+                if (it != c.lower.end()) ch = it->second;
+            }
+        }
         sub_re(c.R("lists"), U"- \\1");
         sub_re(c.R("https"), U"https:");
         {   // '&' -> 'and'
@@ -216,7 +249,10 @@ struct Normalizer {
         strip_re(c.R("developed_by"));
         {
             std::vector<long> caps;
-            if (c.R("end_of_terms").search(cur, 0, caps)) cur.resize((size_t)caps[0]);
+            if (c.R("end_of_terms").search(cur, 0, caps)) {
+                cur.resize((size_t)caps[0]);
+                clean = false;
+            }
         }
         collapse_whitespace();
         strip_re(c.R("mit_optional"));
@@ -282,7 +318,7 @@ void prep_one(const Ctx& c, const char* data, int64_t len, const char* filename,
         content.swap(t);
     }
     for (char32_t ch : content)
-        if (ch >= 0x80 && !safe_nonascii(ch)) { o.status = 1; return; }
+        if (ch >= 0x80 && (c.unicode ? python_only(ch) : !safe_nonascii(ch))) { o.status = 1; return; }
     if (extname_is_html(filename)) { o.status = 1; return; }
     std::vector<long> caps;
     const Str stripped = ruby_strip(content);
@@ -309,7 +345,12 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
     Ctx* c = new Ctx();
     try {
         for (int32_t i = 0; i < n_patterns; ++i) c->re.emplace(names[i], Regex(patterns[i], flags[i]));
-        for (int32_t i = 0; i < n_spell; ++i) c->spell.push_back({rx::from_utf8(spell_from[i]), rx::from_utf8(spell_to[i])});
+        for (int32_t i = 0; i < n_spell; ++i) {
+            c->spell.push_back({rx::from_utf8(spell_from[i]), rx::from_utf8(spell_to[i])});
+            const Str& k = c->spell.back().first;
+            if (k.empty() || k[0] >= 128) throw std::runtime_error("spelling keys must start with an ASCII character");
+            c->spell_first[k[0]].push_back(i);
+        }
         for (int32_t i = 0; i < n_vocab; ++i) c->vocab.emplace(vocab[i], i);
         c->n_vocab = n_vocab;
         c->w64 = (n_vocab + 63) / 64;
@@ -347,6 +388,20 @@ int lh_set_templates(lh_ctx* ctx, int32_t n_templates, const uint64_t* lf_bits, 
 
 // Normalize one text. Returns UTF-8 byte count written to out (NUL-terminated when room),
 // the needed size when cap is too small, -1 when the text needs the Python path.
+int lh_set_unicode(lh_ctx* ctx, int32_t n_lower, const uint32_t* lower_from, const uint32_t* lower_to,
+                   int32_t n_word, const uint32_t* word_lo, const uint32_t* word_hi) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || n_lower < 0 || n_word < 0 || (n_lower && (!lower_from || !lower_to)) || (n_word && (!word_lo || !word_hi)))
+        return -1;
+    for (int32_t i = 1; i < n_word; ++i)
+        if (word_lo[i] <= word_hi[i - 1] || word_lo[i] > word_hi[i]) return -1;
+    c->lower.clear();
+    for (int32_t i = 0; i < n_lower; ++i) c->lower.emplace(lower_from[i], lower_to[i]);
+    rx::set_unicode_word_ranges(word_lo, word_hi, n_word);
+    c->unicode = true;
+    return 0;
+}
+
 int64_t lh_normalize(lh_ctx* ctx, const char* data, int64_t len, const char* filename, int32_t is_file, char* out,
                      int64_t cap) {
     const Ctx* c = reinterpret_cast<const Ctx*>(ctx);

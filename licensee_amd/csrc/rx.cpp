@@ -67,9 +67,28 @@ std::string to_utf8(const Str& s) {
 }
 
 static inline char32_t fold(char32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
-static inline bool is_word(char32_t c) {
-    return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+
+// Python's \w for \b: [A-Za-z0-9_] plus the non-ASCII code points with str.isalnum() True,
+// installed as sorted inclusive ranges by set_unicode_word_ranges (none: ASCII only).
+static std::vector<std::pair<char32_t, char32_t>> g_word_ranges;
+
+void set_unicode_word_ranges(const uint32_t* lo, const uint32_t* hi, int32_t n) {
+    g_word_ranges.clear();
+    for (int32_t i = 0; i < n; ++i) g_word_ranges.push_back({lo[i], hi[i]});
 }
+
+bool is_word_char(char32_t c) {
+    if (c < 128) return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+    size_t a = 0, b = g_word_ranges.size();   // first range with hi >= c
+    while (a < b) {
+        const size_t m = (a + b) / 2;
+        if (g_word_ranges[m].second < c) a = m + 1;
+        else b = m;
+    }
+    return a < g_word_ranges.size() && g_word_ranges[a].first <= c;
+}
+
+static inline bool is_word(char32_t c) { return is_word_char(c); }
 
 // ---- parser ----------------------------------------------------------------------------
 struct Parser {
@@ -448,27 +467,46 @@ static void first_chars(const NodeP& n, std::vector<bool>& set, bool& nonascii, 
     }
 }
 
+// Zero-width anchor every match of n must begin with: Node::BOS (\A), Node::BOL (^) or -1.
+static int lead_anchor(const Node* n) {
+    while (n->kind == Node::GROUP) n = n->kids[0].get();
+    switch (n->kind) {
+        case Node::BOS: return Node::BOS;
+        case Node::BOL: return Node::BOL;
+        case Node::SEQ: return n->kids.empty() ? -1 : lead_anchor(n->kids[0].get());
+        case Node::ALT: {
+            int a = -2;
+            for (auto& k : n->kids) {
+                const int b = lead_anchor(k.get());
+                if (b < 0) return -1;
+                if (a == -2) a = b;
+                else if (a != b) a = Node::BOL;   // \A implies a line start too
+            }
+            return a < 0 ? -1 : a;
+        }
+        default: return -1;
+    }
+}
+
 Regex::Regex(const std::string& utf8, int flags) {
     Parser ps;
     ps.p = from_utf8(utf8);
     root_ = ps.parse_alt((flags & IGNORECASE) != 0, (flags & DOTALL) != 0);
     if (!ps.eof()) throw std::runtime_error("rx parse: unbalanced )");
     ngroups_ = ps.ngroups;
-    // anchored if the first element of the top sequence is \A
-    const Node* r = root_.get();
-    while (r->kind == Node::GROUP && r->group < 0) r = r->kids[0].get();
-    if (r->kind == Node::SEQ && !r->kids.empty()) {
-        const Node* f = r->kids[0].get();
-        while (f->kind == Node::GROUP && f->group < 0) {
-            const Node* g = f->kids[0].get();
-            if (g->kind == Node::SEQ && !g->kids.empty()) f = g->kids[0].get(); else f = g;
-        }
-        anchored_ = f->kind == Node::BOS;
-    }
+    // Where a match can start: \A-led patterns only at position 0, ^-led patterns only at line
+    // starts (every pattern here is re.M). An alternation qualifies when all its branches do.
+    const int lead = lead_anchor(root_.get());
+    anchored_ = lead == Node::BOS;
+    line_anchored_ = lead == Node::BOL;
     std::vector<bool> set(128, false);
     bool nonascii = false, nullable = false;
     first_chars(root_, set, nonascii, nullable);
-    if (!nullable) { first_ = set; first_nonascii_ = nonascii; }
+    if (!nullable) {
+        has_first_ = true;
+        for (int c = 0; c < 128; ++c) first_[c] = set[c] ? 1 : 0;
+        first_nonascii_ = nonascii;
+    }
 }
 
 bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
@@ -479,10 +517,19 @@ bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
     Matcher mt{s, caps};
     for (size_t pos = start; pos <= s.size(); ++pos) {
         if (anchored_ && pos > 0) return false;
-        if (!first_.empty()) {
-            if (pos == s.size()) return false;
-            char32_t c = s[pos];
-            if (c < 128 ? !first_[c] : !first_nonascii_) continue;
+        if (line_anchored_ && pos > 0 && s[pos - 1] != '\n') {
+            // next line start: the character after the next '\n'
+            size_t q = pos;
+            while (q < s.size() && s[q - 1] != '\n') ++q;
+            if (q >= s.size() && !(q == s.size() && s[q - 1] == '\n')) return false;
+            pos = q;
+        }
+        if (has_first_) {
+            // skip to the next character a match can start with
+            const size_t n = s.size();
+            while (pos < n && !(s[pos] < 128 ? first_[s[pos]] : first_nonascii_)) ++pos;
+            if (pos == n) return false;
+            if (line_anchored_ && pos > 0 && s[pos - 1] != '\n') continue;
         }
         if (mt.m(root_.get(), pos, end)) {
             caps[0] = (long)pos;
@@ -491,6 +538,13 @@ bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
         }
     }
     return false;
+}
+
+bool Regex::sub_into(Str& s, const Str& repl) const {
+    std::vector<long> caps;
+    if (!search(s, 0, caps)) return false;
+    s = sub(s, repl);
+    return true;
 }
 
 Str Regex::sub(const Str& s, const Str& repl, bool* changed) const {

@@ -5,8 +5,8 @@
 // scoped flags (?i:) (?-i:)), lookbehind (?<!..) (?<=..) and lookahead (?=..) (?!..) of
 // fixed width, alternation, greedy and lazy quantifiers (* + ? {m,n}), ^ and $ (always
 // multiline here, as every pattern is compiled with re.M). Case-insensitive matching folds
-// ASCII only; callers route text containing non-ASCII letters to the Python path, where
-// Unicode folding could differ (normalize.cpp).
+// ASCII only: the few non-ASCII characters Python's re.I equates with ASCII letters
+// (U+0130, U+0131, U+017F, U+212A) send their text to the Python path (normalize.cpp).
 #pragma once
 
 #include <stdint.h>
@@ -50,6 +50,8 @@ public:
     bool anchored() const { return anchored_; }
     // re.sub with a template supporting \1..\9 (and literal text); count = 0 -> all
     Str sub(const Str& s, const Str& repl, bool* changed = nullptr) const;
+    // in-place re.sub: returns false (s untouched, no copy) when nothing matches
+    bool sub_into(Str& s, const Str& repl) const;
     template <class F>
     Str sub_fn(const Str& s, F&& fn) const;  // replacement computed from the match
     bool valid() const { return (bool)root_; }
@@ -57,14 +59,21 @@ public:
 private:
     NodeP root_;
     int ngroups_ = 0;
-    bool anchored_ = false;           // pattern starts with \A
-    std::vector<bool> first_;         // ASCII first-char filter (empty = any)
-    bool first_nonascii_ = true;
+    bool anchored_ = false;           // every match starts with \A
+    bool line_anchored_ = false;      // every match starts with ^ (a line start)
+    bool has_first_ = false;          // first-character filter active
+    uint8_t first_[128] = {};         // ASCII characters a match can start with
+    bool first_nonascii_ = true;      // ... and whether any non-ASCII one can
     friend struct Matcher;
 };
 
 Str from_utf8(const std::string& s);
 std::string to_utf8(const Str& s);
+
+// \b / \w word characters: ASCII [A-Za-z0-9_] plus the installed non-ASCII ranges (Python's
+// str.isalnum(), supplied by the caller). Process-wide; set once before matching.
+void set_unicode_word_ranges(const uint32_t* lo, const uint32_t* hi, int32_t n);
+bool is_word_char(char32_t c);
 
 }  // namespace rx
 

@@ -3,8 +3,10 @@
 Batched LicenseFile preparation in C++ threads: decode -> content_normalized -> wordset ->
 vocabulary bitset, plus the CC flag, the Copyright matcher and the Exact matcher. The regular
 expressions are exactly the compiled patterns of ``content_helper.py`` (handed over here),
-so the two host paths share one pattern source; texts the native path does not cover
-(non-ASCII letters, HTML) fall back to the Python path per file.
+so the two host paths share one pattern source, and Python's own Unicode tables
+(``unicode_tables``: lower-casing, ``\\w``) so non-ASCII text stays native. Texts the native
+path does not cover (HTML; the five characters whose Python semantics are contextual, see
+normalize.cpp ``python_only``) fall back to the Python path per file.
 """
 from __future__ import annotations
 
@@ -38,8 +40,43 @@ def _load():
         l.lh_normalize.argtypes = [vp, ctypes.c_char_p, i64, ctypes.c_char_p, i32, ctypes.c_char_p, i64]
         l.lh_prep_files.restype = ctypes.c_int
         l.lh_prep_files.argtypes = [vp, i64, cpp, vp, cpp, i32, vp, vp, vp, vp, vp, vp, vp]
+        l.lh_set_unicode.restype = ctypes.c_int
+        l.lh_set_unicode.argtypes = [vp, i32, vp, vp, i32, vp, vp]
         _lib = l
     return _lib
+
+
+_UNICODE = None
+
+
+def unicode_tables():
+    """Python's own per-character semantics the native normalizer needs for non-ASCII text:
+    (lower_from, lower_to) for every code point whose ``str.lower()`` is a different single
+    code point, and the inclusive ranges of non-ASCII code points with ``str.isalnum()``
+    (``re``'s Unicode ``\\w``, which decides ``\\b``)."""
+    global _UNICODE
+    if _UNICODE is None:
+        import sys
+        frm, to, lo, hi = [], [], [], []
+        start = None
+        for cp in range(128, sys.maxunicode + 1):
+            ch = chr(cp)
+            low = ch.lower()
+            if low != ch and len(low) == 1:
+                frm.append(cp)
+                to.append(ord(low))
+            if ch.isalnum():
+                if start is None:
+                    start = cp
+            elif start is not None:
+                lo.append(start)
+                hi.append(cp - 1)
+                start = None
+        if start is not None:
+            lo.append(start)
+            hi.append(sys.maxunicode)
+        _UNICODE = tuple(np.array(a, np.uint32) for a in (frm, to, lo, hi))
+    return _UNICODE
 
 
 def _cstrs(items: Sequence[Union[str, bytes]]):
@@ -82,6 +119,11 @@ class HostPrep:
                                 len(vocab), vw, err, 512)
         if not self._c:
             raise RuntimeError('lh_create failed: ' + err.value.decode())
+        self._uni = unicode_tables()
+        lf, lt, wl, wh = self._uni
+        if lib.lh_set_unicode(self._c, len(lf), lf.ctypes.data, lt.ctypes.data, len(wl), wl.ctypes.data,
+                              wh.ctypes.data) != 0:
+            raise RuntimeError('lh_set_unicode rejected the tables')
         self.corpus = corpus
         if corpus is not None:
             tpl = corpus.templates
