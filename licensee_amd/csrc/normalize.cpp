@@ -42,16 +42,6 @@ Str ruby_strip(const Str& s) {
     return s.substr(a, b - a);
 }
 
-Str squeeze_spaces(const Str& s) {
-    Str out;
-    out.reserve(s.size());
-    for (size_t i = 0; i < s.size(); ++i) {
-        if (s[i] == kSpace && !out.empty() && out.back() == kSpace) continue;
-        out.push_back(s[i]);
-    }
-    return out;
-}
-
 bool contains(const Str& s, const char* lit) {
     Str l = rx::from_utf8(lit);
     return s.find(l) != Str::npos;
@@ -101,10 +91,25 @@ struct Normalizer {
     Str cur;
     bool clean = false;   // cur is already squeezed and stripped (a strip op without a match is a no-op)
 
+    // squeeze(' ').strip in place (String#squeeze / #strip: only ' ' runs, \0\t\n\v\f\r ends)
+    void squeeze_strip() {
+        size_t w = 0;
+        for (size_t r = 0; r < cur.size(); ++r) {
+            if (cur[r] == kSpace && w > 0 && cur[w - 1] == kSpace) continue;
+            cur[w++] = cur[r];
+        }
+        cur.resize(w);
+        size_t b = cur.size();
+        while (b > 0 && is_strip_char(cur[b - 1])) --b;
+        cur.resize(b);
+        size_t a = 0;
+        while (a < cur.size() && is_strip_char(cur[a])) ++a;
+        if (a) cur.erase(0, a);
+    }
     // strip(re): gsub(re, ' ').squeeze(' ').strip (content_helper.rb:223-236)
     void strip_re(const Regex& r) {
         if (!r.sub_into(cur, U" ") && clean) return;
-        cur = ruby_strip(squeeze_spaces(cur));
+        squeeze_strip();
         clean = true;
     }
     void sub_re(const Regex& r, const char32_t* repl) {
@@ -153,10 +158,13 @@ struct Normalizer {
     // path has ASCII word characters only, so \b is the ASCII boundary.
     void spelling() {
         const size_t n = cur.size();
-        auto word = [](char32_t ch) { return rx::is_word_char(ch); };   // Python \b's \w
+        auto word = [](char32_t ch) {   // Python \b's \w
+            return ch < 128 ? ((ch | 32) >= 'a' && (ch | 32) <= 'z') || (ch >= '0' && ch <= '9') || ch == '_'
+                            : rx::is_word_char(ch);
+        };
         // the replacement of the key matching at word start i, or nullptr
         auto match_at = [&](size_t i, size_t& klen) -> const Str* {
-            if (cur[i] >= 128 || !word(cur[i]) || (i > 0 && word(cur[i - 1]))) return nullptr;
+            if (cur[i] >= 128 || c.spell_first[cur[i]].empty() || (i > 0 && word(cur[i - 1]))) return nullptr;
             for (int si : c.spell_first[cur[i]]) {
                 const Str& k = c.spell[si].first;
                 if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 && (i + k.size() == n || !word(cur[i + k.size()]))) {
@@ -185,16 +193,20 @@ struct Normalizer {
         clean = false;
     }
 
-    // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip
+    // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip, in place
     void collapse_whitespace() {
-        Str out;
-        out.reserve(cur.size());
-        for (char32_t ch : cur) {
+        size_t w = 0;
+        for (size_t r = 0; r < cur.size(); ++r) {
+            const char32_t ch = cur[r];
             const bool ws = ch == ' ' || (ch >= '\t' && ch <= '\r');
-            if (ws) { if (out.empty() || out.back() != ' ') out.push_back(' '); }
-            else out.push_back(ch);
+            if (ws) {
+                if (w == 0 || cur[w - 1] != ' ') cur[w++] = ' ';
+            } else {
+                cur[w++] = ch;
+            }
         }
-        cur = ruby_strip(out);
+        cur.resize(w);
+        squeeze_strip();
         clean = true;
     }
 
