@@ -25,7 +25,7 @@ from ._native import FileBatch, words64
 
 _HOST_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib', 'liblicensee_host.so')
 _CACHE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib', 'cache')
-_PACK_VERSION = 1
+_PACK_VERSION = 2
 _packed: Dict[str, np.ndarray] = {}
 
 
@@ -63,61 +63,129 @@ def vocabulary_order(members: Dict[str, List[int]], n_templates: int) -> List[st
 
 
 def _pack_budget(n_vocab: int, n_templates: int) -> int:
-    """Local-search attempts: ~3 s for the 47 vendored templates, ~15 s for ~600 templates."""
+    """Default local-search attempts: ~3 s for the 47 vendored templates, ~15 s for ~600."""
     return n_vocab * (10000 if n_templates <= 64 else 2000)
 
 
-def pack_vocabulary(order: List[str], members: Dict[str, List[int]], n_templates: int) -> List[str]:
+def _pack_lib():
+    try:
+        lib = ctypes.CDLL(_HOST_LIB)
+    except OSError:
+        return None
+    fn = lib.lh_vocab_pack
+    fn.restype = ctypes.c_int64
+    vp = ctypes.c_void_p
+    fn.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int64,
+                   ctypes.c_uint64, vp]
+    return fn
+
+
+def _signatures(order: List[str], members: Dict[str, List[int]], n_templates: int) -> np.ndarray:
+    W = (n_templates + 63) // 64
+    sig = np.zeros((len(order), W), np.uint64)
+    for i, w in enumerate(order):
+        for t in members[w]:
+            sig[i, t >> 6] |= np.uint64(1) << np.uint64(t & 63)
+    return sig
+
+
+def _cache_path(sig: np.ndarray, n_templates: int, bin_bits: int) -> str:
+    key = hashlib.sha1(sig.tobytes() + struct.pack('<iiii', sig.shape[0], n_templates, bin_bits,
+                                                   _PACK_VERSION)).hexdigest()[:20]
+    return os.path.join(_CACHE_DIR, f'vocab_{key}.i32')
+
+
+def _read_perm(path: str, V: int):
+    if not os.path.exists(path):
+        return None
+    perm = np.fromfile(path, dtype=np.int32)
+    if len(perm) != V or not np.array_equal(np.sort(perm), np.arange(V, dtype=np.int32)):
+        return None
+    return perm
+
+
+def _write_perm(path: str, perm: np.ndarray):
+    try:
+        os.makedirs(_CACHE_DIR, exist_ok=True)
+        tmp = f'{path}.{os.getpid()}'
+        perm.tofile(tmp)
+        os.replace(tmp, path)
+    except OSError:
+        pass
+
+
+def pack_vocabulary(order: List[str], members: Dict[str, List[int]], n_templates: int,
+                    iters: int = None) -> List[str]:
     """Re-pack ``order`` into device bins with the native local search (lh_vocab_pack).
 
     Bins are 32 words for the sparse program (T <= 64: cost = instruction pairs per
     (template, dword)) and 64 words for the LDS kernel (records per (template, u64)).
-    Measured: 1347 -> ~1090 program entries on the 47 vendored templates (-7% kernel time,
-    config 2) and 76.7k -> ~51k records at T = 600. Deterministic (fixed seed); results are
-    cached in-process and under lib/cache by a hash of the signatures. Without the native
-    host library the order is returned unchanged (scores do not depend on the order)."""
+    Deterministic (fixed seed). The result is cached in-process and under lib/cache by a
+    hash of the signatures; a cached order is used as is, so a longer build-time search
+    (:func:`improve_packing`) serves every later run. Without the native host library the
+    order is returned unchanged (scores never depend on the order)."""
     V = len(order)
     if V < 2 or n_templates < 2:   # one template: every word has the same signature
         return order
-    W = (n_templates + 63) // 64
-    sig = np.zeros((V, W), np.uint64)
-    for i, w in enumerate(order):
-        for t in members[w]:
-            sig[i, t >> 6] |= np.uint64(1) << np.uint64(t & 63)
+    sig = _signatures(order, members, n_templates)
     bin_bits = 32 if n_templates <= 64 else 64
-    iters = _pack_budget(V, n_templates)
-    key = hashlib.sha1(sig.tobytes() + struct.pack('<iiiqi', V, n_templates, bin_bits, iters, _PACK_VERSION)).hexdigest()[:20]
-    perm = _packed.get(key)
-    path = os.path.join(_CACHE_DIR, f'vocab_{key}.i32')
-    if perm is None and os.path.exists(path):
-        perm = np.fromfile(path, dtype=np.int32)
-        if len(perm) != V or not np.array_equal(np.sort(perm), np.arange(V, dtype=np.int32)):
-            perm = None
+    path = _cache_path(sig, n_templates, bin_bits)
+    perm = _packed.get(path)
     if perm is None:
-        try:
-            lib = ctypes.CDLL(_HOST_LIB)
-        except OSError:
+        perm = _read_perm(path, V)
+    if perm is None:
+        fn = _pack_lib()
+        if fn is None:
             print(f'licensee_amd: {_HOST_LIB} missing, vocabulary left unpacked', file=sys.stderr)
             return order
-        fn = lib.lh_vocab_pack
-        fn.restype = ctypes.c_int64
-        vp = ctypes.c_void_p
-        fn.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int64,
-                       ctypes.c_uint64, vp]
         init = np.arange(V, dtype=np.int32)
-        out = np.empty(V, np.int32)
-        if fn(sig.ctypes.data, V, W, n_templates, init.ctypes.data, bin_bits, iters, 20250202, out.ctypes.data) < 0:
+        perm = np.empty(V, np.int32)
+        budget = _pack_budget(V, n_templates) if iters is None else iters
+        if fn(sig.ctypes.data, V, sig.shape[1], n_templates, init.ctypes.data, bin_bits, budget, 20250202,
+              perm.ctypes.data) < 0:
             raise ValueError('lh_vocab_pack rejected the vocabulary')
-        perm = out
-        try:
-            os.makedirs(_CACHE_DIR, exist_ok=True)
-            tmp = f'{path}.{os.getpid()}'
-            perm.tofile(tmp)
-            os.replace(tmp, path)
-        except OSError:
-            pass
-    _packed[key] = perm
+        _write_perm(path, perm)
+    _packed[path] = perm
     return [order[i] for i in perm]
+
+
+def improve_packing(templates: Sequence, iters_per_word: int) -> Tuple[int, int]:
+    """Build step: continue the local search from the cached order of ``templates``' corpus
+    with a larger budget and keep the result when it is cheaper. Returns (old, new) cost."""
+    lfs = [t.wordset_fieldless() for t in templates]
+    members: Dict[str, List[int]] = {}
+    for i, lf in enumerate(lfs):
+        for w in lf:
+            members.setdefault(w, []).append(i)
+    T = len(lfs)
+    order = vocabulary_order(members, T)
+    V = len(order)
+    fn = _pack_lib()
+    if fn is None or V < 2 or T < 2:
+        return 0, 0
+    pack_vocabulary(order, members, T)                  # make sure a cached order exists
+    sig = _signatures(order, members, T)
+    bin_bits = 32 if T <= 64 else 64
+    path = _cache_path(sig, T, bin_bits)
+    marker = f'{path}.improved{iters_per_word}'
+    cur = _read_perm(path, V)
+    if cur is None:
+        cur = _packed[path]
+    out = np.empty(V, np.int32)
+    if os.path.exists(marker):                          # already searched with this budget
+        c = fn(sig.ctypes.data, V, sig.shape[1], T, cur.ctypes.data, bin_bits, 0, 1, out.ctypes.data)
+        return c, c
+    old = fn(sig.ctypes.data, V, sig.shape[1], T, cur.ctypes.data, bin_bits, 0, 1, out.ctypes.data)
+    new = fn(sig.ctypes.data, V, sig.shape[1], T, cur.ctypes.data, bin_bits, V * iters_per_word, 20250202,
+             out.ctypes.data)
+    if 0 <= new < old:
+        _write_perm(path, out)
+        _packed[path] = out
+    try:
+        open(marker, 'w').close()
+    except OSError:
+        pass
+    return old, min(old, new) if new >= 0 else old
 
 
 class TemplateCorpus:

@@ -53,7 +53,9 @@ typedef long long i64;
 // v_mul_u32_u24: full-rate 24x24 multiply (low 32 bits); v_sad_u32: |a - b| + c in one op.
 __device__ __forceinline__ u32 mul24(u32 a, u32 b) { u32 r; asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
 __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { u32 r; asm("v_sad_u32 %0, %1, %2, 0" : "=v"(r) : "s"(a), "v"(b)); return r; }
+__device__ __forceinline__ u32 subsat(u32 a, u32 b) { return __builtin_elementwise_sub_sat(a, b); }   // v_sub_u32 clamp
 #else
+__device__ __forceinline__ u32 subsat(u32 a, u32 b) { return a > b ? a - b : 0u; }
 __device__ __forceinline__ u32 mul24(u32 a, u32 b) { return (a & 0xffffffu) * (b & 0xffffffu); }
 __device__ __forceinline__ u32 absdiff(u32 a, u32 b) { return a > b ? a - b : b - a; }
 #endif
@@ -86,11 +88,12 @@ __device__ __forceinline__ uint4 ldq(const uint4* p) { return *p; }
 #endif
 // Denominator (content_helper.rb:130-132,337-347); lengths are non-negative (len_F < 2^31).
 __device__ __forceinline__ i32 dn(i32 base, i32 slack, i32 tlen, u32 wf, i32 lf) {
-    const i32 d = (i32)absdiff((u32)tlen, (u32)lf);
-    i32 adj = slack < 0 ? d : (d - slack > 0 ? d - slack : 0);
-    return base + (i32)wf + adj / 4;
+    const u32 d = absdiff((u32)tlen, (u32)lf);
+    const u32 adj = slack <= 0 ? d : subsat(d, (u32)slack);   // max(d - slack, 0)
+    return base + (i32)wf + (i32)(adj >> 2);
 }
 __device__ __forceinline__ double sc(u32 o, i32 d) { return ((double)o * 200.0) / (double)d; }
+// Overlaps may carry a template index in bits 24-31 (match kernel): only bits 0-23 count.
 template <bool FAST>
 __device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
     if (FAST) {
@@ -98,10 +101,10 @@ __device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
         // ov < 2^11 and den < 2^21: both products < 2^32, full-rate 24-bit multiplies are exact
         return mul24(oa, (u32)db) >= mul24(ob, (u32)da);
 #else
-        return (u64)oa * (u64)(u32)db >= (u64)ob * (u64)(u32)da;
+        return (u64)(oa & 0xFFFFFFu) * (u64)(u32)db >= (u64)(ob & 0xFFFFFFu) * (u64)(u32)da;
 #endif
     }
-    return sc(oa, da) >= sc(ob, db);
+    return sc(oa & 0xFFFFFFu, da) >= sc(ob & 0xFFFFFFu, db);
 }
 #define ACC(d, m) a = __builtin_popcount(f[d] & (m##u)) + a
 #define ACCF(d) a = __builtin_popcount(f[d]) + a
@@ -122,16 +125,19 @@ extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
     const bool cc = ccp[file] != 0;
     FILE_PROLOGUE
     const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
-    i32 bi = -1; u32 bo = 0; i32 bd = 1;
+    // running best: bo = template index << 24 | overlap (0xFF: none yet), bd = its denominator
+    u32 bo = 0xFF000000u; i32 bd = 1;
     if (__all(fast)) {
         MATCH_BODY(true)
     } else {
         MATCH_BODY(false)
     }
     if (file < n) {
-        const double s = bi >= 0 ? sc(bo, bd) : 0.0;
+        const i32 bi = (bo >> 24) == 0xFFu ? -1 : (i32)(bo >> 24);
+        const u32 bov = bo & 0xFFFFFFu;
+        const double s = bi >= 0 ? sc(bov, bd) : 0.0;
         best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
-        ov_out[file] = bo;
+        ov_out[file] = bov;
         score_out[file] = s;
     }
 }
@@ -377,7 +383,9 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     auto offer = [&](int32_t i) {
         std::ostringstream o;
         if (t->is_cc[i]) o << "if (!cc) ";
-        o << "{ if ((!FASTV && bi < 0) || ge<FASTV>(a, d, bo, bd)) { bi = " << i << "; bo = a; bd = d; } }";
+        // a carries the template index in its top byte (ACC_INIT): one select moves index and
+        // overlap together; v_mul_u32_u24 reads only the low 24 bits (the overlap)
+        o << "{ if ((!FASTV && (bo >> 24) == 0xFFu) || ge<FASTV>(a, d, bo, bd)) { bo = a; bd = d; } }";
         return o.str();
     };
     std::ostringstream match_body, matrix_body, prologue;
@@ -387,7 +395,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         size_t e = 0;
         for (int32_t i = 0; i < t->n_templates; ++i) {
             std::ostringstream acc;
-            acc << "a = 0; ";
+            acc << "a = ACC_INIT(" << i << "); ";
             for (; e < p.prog.size() && p.prog[e].tpl == i; ++e) {
                 const Entry& en = p.prog[e];
                 if (en.mask == 0xFFFFFFFFu) acc << "ACCF(" << en.dword << "); ";
@@ -402,7 +410,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         std::stable_sort(dm.begin(), dm.end(), [](const Entry& x, const Entry& y) {
             return x.dword != y.dword ? x.dword < y.dword : x.tpl < y.tpl;
         });
-        prologue << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = 0;\n";
+        prologue << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = ACC_INIT(i);\n";
         // quads the program touches, in order
         std::vector<int32_t> quads;
         for (const Entry& en : dm)
@@ -474,7 +482,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         match_body.str(mb.str());
     }
     emit_macro(s, "MATCH_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", match_body.str() + "}");
-    s << kMatchKernel;
+    s << "#define ACC_INIT(i) ((u32)(i) << 24)\n" << kMatchKernel << "#undef ACC_INIT\n#define ACC_INIT(i) 0u\n";
     s << kMatrixOffer;
     emit_macro(s, "MATRIX_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", matrix_body.str() + "}");
     for (int km : {4, 16}) {
