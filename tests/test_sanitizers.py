@@ -1,0 +1,94 @@
+"""The native host library under AddressSanitizer + UndefinedBehaviorSanitizer.
+
+tests/sanitize/driver.cpp links csrc/rx.cpp, normalize.cpp and vocab_pack.cpp built with
+-fsanitize=address,undefined (no recovery) and drives every entry point of
+include/licensee_host.h -- lh_create, lh_set_unicode, lh_set_templates, threaded
+lh_prep_files, lh_normalize, lh_vocab_pack, lh_destroy -- over the reference fixture texts
+(goldens), all 47 template texts, seeded fuzz texts (markup, non-ASCII, contextual
+characters) and long mixed files. Host code only: GPU sanitizers are not available.
+"""
+import json
+import os
+import random
+import shutil
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _s(b: bytes) -> bytes:
+    return struct.pack('<I', len(b)) + b
+
+
+def _strs(items) -> bytes:
+    out = struct.pack('<I', len(items))
+    for x in items:
+        out += _s(x if isinstance(x, bytes) else x.encode('utf-8'))
+    return out
+
+
+def _arr(a: np.ndarray) -> bytes:
+    a = np.ascontiguousarray(a)
+    return struct.pack('<I', a.size) + a.tobytes()
+
+
+def _texts():
+    from licensee_amd.license import License
+    from tests.test_native_host import CONTEXTUAL, FRAGMENTS
+    with open(os.path.join(HERE, 'golden', 'vendored.json'), encoding='utf-8') as fh:
+        vend = json.load(fh)
+    texts = [c['normalized'] for t in vend['templates'] for c in t['cases'].values()]
+    texts += [l.content_normalized() for l in License.all(hidden=True, pseudo=False)]
+    rng = random.Random(7)
+    for _ in range(300):
+        parts = [rng.choice(FRAGMENTS + CONTEXTUAL) for _ in range(rng.randint(1, 15))]
+        texts.append(rng.choice(['\n', '\n\n', ' ', '\r\n']).join(parts))
+    bodies = [l.content_normalized() for l in License.all(hidden=True, pseudo=False)]
+    texts += ['\n\n'.join(rng.sample(bodies, 4)) for _ in range(10)]           # long mixed files
+    texts += ['', ' ', '\n', '﻿', 'x' * 5000, '[' * 300 + ']' * 300, '- ' * 2000]
+    return [t.encode('utf-8') for t in texts] + [b'\xff\xfe invalid \xc3', b'\xe2\x80']
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+def test_host_library_under_asan_ubsan(tmp_path):
+    from licensee_amd import content_helper as ch
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from licensee_amd.native_host import _FLAG_MASK, host_patterns, unicode_tables
+    corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    pats = host_patterns()
+    fields, off = [], [0]
+    for t in corpus.templates:
+        fields.extend(sorted(set(t.fields_normalized())))
+        off.append(len(fields))
+    lf, lt, wl, wh = unicode_tables()
+    T = len(corpus.templates)
+    sig = np.zeros((corpus.n_vocab, 1), np.uint64)
+    bits = np.unpackbits(corpus.lf_bits.view(np.uint8).reshape(T, -1), axis=1, bitorder='little')[:, :corpus.n_vocab]
+    for t in range(T):
+        sig[:, 0] |= bits[t].astype(np.uint64) << np.uint64(t)
+    blob = (_strs(list(pats)) + _strs([p.pattern for p in pats.values()]) +
+            _arr(np.array([p.flags & _FLAG_MASK for p in pats.values()], np.int32)) +
+            _strs(list(ch.VARIETAL_WORDS)) + _strs(list(ch.VARIETAL_WORDS.values())) + _strs(corpus.vocab) +
+            struct.pack('<I', T) + _arr(corpus.lf_bits) +
+            _arr(np.array([len(t.wordset()) for t in corpus.templates], np.uint32)) +
+            _arr(np.array(off, np.int32)) + _strs(fields) +
+            _arr(lf) + _arr(lt) + _arr(wl) + _arr(wh) + _strs(_texts()) + _arr(sig) + struct.pack('<I', 1))
+    inp = tmp_path / 'input.bin'
+    inp.write_bytes(blob)
+    exe = str(tmp_path / 'drv')
+    csrc = os.path.join(ROOT, 'licensee_amd', 'csrc')
+    subprocess.run(['g++', '-std=c++17', '-O1', '-g', '-fno-omit-frame-pointer', '-fsanitize=address,undefined',
+                    '-fno-sanitize-recover=all', '-pthread', '-I', os.path.join(ROOT, 'include'), '-I', csrc,
+                    '-o', exe, os.path.join(HERE, 'sanitize', 'driver.cpp'), os.path.join(csrc, 'rx.cpp'),
+                    os.path.join(csrc, 'normalize.cpp'), os.path.join(csrc, 'vocab_pack.cpp')], check=True)
+    env = dict(os.environ, ASAN_OPTIONS='detect_leaks=1:abort_on_error=1', UBSAN_OPTIONS='print_stacktrace=1')
+    r = subprocess.run([exe, str(inp)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert r.stdout.startswith('ok '), r.stdout
+    assert 'runtime error' not in r.stderr and 'AddressSanitizer' not in r.stderr, r.stderr[-4000:]
