@@ -323,8 +323,8 @@ static std::string acc_block(const std::vector<Entry>& dm, size_t b, size_t e) {
 
 // Accumulations of one quad, in blocks of at most kAccBlock entries.
 static std::string acc_quad(const std::vector<Entry>& dm, size_t& e, int32_t q) {
-    const char* be = getenv("DICE_PROG_ACC_BLOCK");   // entries per asm block (A/B runs)
-    const size_t kAccBlock = be && *be ? (size_t)std::max(1, std::min(16, atoi(be))) : 8;
+    const char* be = getenv("DICE_PROG_ACC_BLOCK");   // entries per asm block (4 measured best)
+    const size_t kAccBlock = be && *be ? (size_t)std::max(1, std::min(16, atoi(be))) : 4;
     size_t end = e;
     while (end < dm.size() && dm[end].dword / 4 == q) ++end;
     std::string out;
@@ -437,10 +437,11 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         } else {
             // bursts (default): quads in groups of `nb`, double-buffered in register sets
             // p0_* / p1_*; group g+1 is requested (nb contiguous 1 KiB wave loads back to back)
-            // before group g is consumed. With non-temporal loads, nb = 3 measured ~1.5% ahead
-            // of the 8-deep ring at 92 instead of 124 VGPRs (same box, interleaved A/B runs).
+            // before group g is consumed. With non-temporal loads, bursts of 3 measured ~1.5% ahead
+            // of the 8-deep ring at 92 instead of 124 VGPRs, bursts of 4 (96 VGPRs) with 4-entry asm
+            // blocks another ~3.5% (same box, interleaved A/B runs, tools/gpu_ab_prog.sh).
             const char* b_env = getenv("DICE_PROG_BURST");
-            int nb = b_env && *b_env ? atoi(b_env) : 3;
+            int nb = b_env && *b_env ? atoi(b_env) : 4;
             nb = std::max(1, std::min<int>(nb, (int)quads.size()));
             const size_t ng = (quads.size() + nb - 1) / nb;
             auto group_loads = [&](std::ostringstream& o, size_t g, int set) {
