@@ -441,7 +441,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             // of the 8-deep ring at 92 instead of 124 VGPRs, bursts of 4 (96 VGPRs) with 4-entry asm
             // blocks another ~3.5% (same box, interleaved A/B runs, tools/gpu_ab_prog.sh).
             const char* b_env = getenv("DICE_PROG_BURST");
-            int nb = b_env && *b_env ? atoi(b_env) : 4;
+            int nb = b_env && *b_env ? atoi(b_env) : 5;
             nb = std::max(1, std::min<int>(nb, (int)quads.size()));
             const size_t ng = (quads.size() + nb - 1) / nb;
             auto group_loads = [&](std::ostringstream& o, size_t g, int set) {
