@@ -365,6 +365,12 @@ class ContentHelper:
     def has_spdx_alt_segments(self) -> bool:
         return hasattr(self, 'spdx_alt_segments')
 
+    def similarity(self, other) -> float:
+        """content_helper.rb:128-133 for any two ContentHelper objects, scored on the GPU
+        (``dice.pair_similarity``); a non-License self uses the simple length delta (:343)."""
+        from .dice import pair_similarity
+        return pair_similarity(self, other)
+
     def variation_adjusted_length_delta(self, other) -> int:
         """content_helper.rb:337-347"""
         delta = self.length_delta(other)

@@ -66,6 +66,27 @@ def test_dice_matcher_spec():
     assert mit.similarity(mit) == 100.0
 
 
+def test_content_helper_spec_similarity():
+    """content_helper_spec.rb:68-75 with the spec's test helper (not a License: simple length
+    delta, :343): mit.similarity(h) ~ 4, h.similarity(mit) ~ 3, mit.similarity(mit) == 100.0 --
+    and both equal to the formula evaluated on the host sets (content_helper.rb:128-133)."""
+    from tests.test_normalize import SPEC_CONTENT, Helper
+    h = Helper(SPEC_CONTENT, 'license.md')
+    mit = License.find('mit')
+
+    def formula(a, b, simple):
+        ov = len(a.wordset_fieldless() & b.wordset())
+        total = len(a.wordset_fieldless()) + len(b.wordset()) - len(a.fields_normalized_set())
+        delta = abs(a.length() - b.length())
+        if not simple:
+            delta = max(delta - 5 * max(len(a.fields_normalized()), a.spdx_alt_segments()), 0)
+        return (ov * 200.0) / (total + delta // 4)
+    s1, s2 = mit.similarity(h), h.similarity(mit)
+    assert abs(s1 - 4) <= 1 and abs(s2 - 3) <= 1
+    assert s1 == formula(mit, h, False) and s2 == formula(h, mit, True)
+    assert mit.similarity(mit) == 100.0
+
+
 def test_fixture_expectations_on_gpu():
     recs = golden('fixture_files.json')
     singles = [r for r in recs if sum(x['fixture'] == r['fixture'] for x in recs) == 1
