@@ -22,7 +22,9 @@ from .license import License
 class DiceEngine:
     def __init__(self, templates: Optional[Sequence[License]] = None, device: int = 0):
         self.templates = list(templates) if templates is not None else License.all(hidden=True, pseudo=False)
-        self.position = {t.key: i for i, t in enumerate(self.templates)}
+        # key order positions (License objects); any other ContentHelper self (pair_similarity)
+        # has no key and is only addressed by index
+        self.position = {getattr(t, 'key', f'#{i}'): i for i, t in enumerate(self.templates)}
         self.corpus = TemplateCorpus(self.templates)
         c = self.corpus
         self.scorer = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc,
