@@ -284,7 +284,9 @@ def main():
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'traffic_source': traffic_src,
-                         'algorithmic_bytes_per_file': algo_bytes_per_file, 'launch_ms': launch_ms},
+                         'algorithmic_bytes_per_file': algo_bytes_per_file, 'launch_ms': launch_ms,
+                         **({'note': 'config 3 is compute-bound (VALU/LDS issue of the LDS-tiled kernel); '
+                                     'frac is its HBM share only (DESIGN.md 4b)'} if kind == 2 else {})},
             'cpu_baseline': cpu_baseline,
             'scores_per_s': value * T,
             'parity': parity,
