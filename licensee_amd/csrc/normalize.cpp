@@ -162,33 +162,42 @@ struct Normalizer {
             return ch < 128 ? ((ch | 32) >= 'a' && (ch | 32) <= 'z') || (ch >= '0' && ch <= '9') || ch == '_'
                             : rx::is_word_char(ch);
         };
-        // the replacement of the key matching at word start i, or nullptr
-        auto match_at = [&](size_t i, size_t& klen) -> const Str* {
-            if (cur[i] >= 128 || c.spell_first[cur[i]].empty() || (i > 0 && word(cur[i - 1]))) return nullptr;
-            for (int si : c.spell_first[cur[i]]) {
-                const Str& k = c.spell[si].first;
-                if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 && (i + k.size() == n || !word(cur[i + k.size()]))) {
-                    klen = k.size();
-                    return &c.spell[si].second;
+        // next hit at or after i: only word starts are candidates (every key starts with a
+        // letter, so \b(?:key) can only match there); skips whole words otherwise
+        auto next_hit = [&](size_t i, size_t& at, size_t& klen) -> const Str* {
+            while (i < n) {
+                const char32_t ch = cur[i];
+                if (!word(ch)) {
+                    ++i;
+                    continue;
                 }
+                if (ch < 128)
+                    for (int si : c.spell_first[ch]) {
+                        const Str& k = c.spell[si].first;
+                        if (k.size() <= n - i && cur[i + 1] == k[1] && cur.compare(i, k.size(), k) == 0 &&
+                            (i + k.size() == n || !word(cur[i + k.size()]))) {
+                            at = i;
+                            klen = k.size();
+                            return &c.spell[si].second;
+                        }
+                    }
+                while (i < n && word(cur[i])) ++i;
             }
             return nullptr;
         };
-        size_t i = 0, klen = 0;
-        const Str* rep = nullptr;
-        while (i < n && !(rep = match_at(i, klen))) ++i;
+        size_t at = 0, klen = 0;
+        const Str* rep = next_hit(0, at, klen);
         if (!rep) return;   // no varietal word: nothing to rebuild
-        Str out(cur, 0, i);
+        Str out;
         out.reserve(n);
-        while (i < n) {
-            if (rep) {
-                out += *rep;
-                i += klen;
-            } else {
-                out.push_back(cur[i++]);
-            }
-            rep = i < n ? match_at(i, klen) : nullptr;
+        size_t i = 0;
+        while (rep) {
+            out.append(cur, i, at - i);
+            out += *rep;
+            i = at + klen;
+            rep = next_hit(i, at, klen);
         }
+        out.append(cur, i, Str::npos);
         cur.swap(out);
         clean = false;
     }
@@ -360,7 +369,7 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
         for (int32_t i = 0; i < n_spell; ++i) {
             c->spell.push_back({rx::from_utf8(spell_from[i]), rx::from_utf8(spell_to[i])});
             const Str& k = c->spell.back().first;
-            if (k.empty() || k[0] >= 128) throw std::runtime_error("spelling keys must start with an ASCII character");
+            if (k.size() < 2 || k[0] >= 128) throw std::runtime_error("spelling keys: >= 2 characters, ASCII first");
             c->spell_first[k[0]].push_back(i);
         }
         for (int32_t i = 0; i < n_vocab; ++i) c->vocab.emplace(vocab[i], i);
