@@ -322,20 +322,13 @@ static std::string acc_block(const std::vector<Entry>& dm, size_t b, size_t e) {
 }
 
 // Accumulations of one quad, in blocks of at most kAccBlock entries.
-static std::string acc_quad(const std::vector<Entry>& dm, size_t& e, int32_t q) {
+static std::string acc_quad(const std::vector<Entry>& dm, size_t b0, size_t end, int32_t q) {
     const char* be = getenv("DICE_PROG_ACC_BLOCK");   // entries per asm block (4 measured best)
     const size_t kAccBlock = be && *be ? (size_t)std::max(1, std::min(16, atoi(be))) : 4;
-    size_t end = e;
-    while (end < dm.size() && dm[end].dword / 4 == q) ++end;
     std::string out;
     const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
-    if (diag && strcmp(diag, "noacc") == 0) {
-        out = "acc[" + std::to_string(q) + " % NT] ^= f[0] ^ f[1] ^ f[2] ^ f[3];\n";
-        e = end;
-        return out;
-    }
-    for (size_t b = e; b < end; b += kAccBlock) out += acc_block(dm, b, std::min(end, b + kAccBlock));
-    e = end;
+    if (diag && strcmp(diag, "noacc") == 0) return "acc[" + std::to_string(q) + " % NT] ^= f[0] ^ f[1] ^ f[2] ^ f[3];\n";
+    for (size_t b = b0; b < end; b += kAccBlock) out += acc_block(dm, b, std::min(end, b + kAccBlock));
     return out;
 }
 
@@ -411,10 +404,70 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             return x.dword != y.dword ? x.dword < y.dword : x.tpl < y.tpl;
         });
         prologue << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = ACC_INIT(i);\n";
-        // quads the program touches, in order
+        // quads the program touches, their entry ranges in dm and their VALU cost
         std::vector<int32_t> quads;
-        for (const Entry& en : dm)
-            if (quads.empty() || quads.back() != en.dword / 4) quads.push_back(en.dword / 4);
+        std::vector<std::pair<size_t, size_t>> range;   // [begin, end) in dm, per quads[] slot
+        std::vector<int> cost;
+        for (size_t i = 0; i < dm.size(); ++i) {
+            if (quads.empty() || quads.back() != dm[i].dword / 4) {
+                quads.push_back(dm[i].dword / 4);
+                range.push_back({i, i});
+                cost.push_back(0);
+            }
+            range.back().second = i + 1;
+            cost.back() += dm[i].mask == 0xFFFFFFFFu ? 1 : 2;
+        }
+        {   // processing order (DICE_PROG_QORDER): "asc" memory order; "desc" costliest quads
+            // first, so a wave's heavy accumulate work overlaps its later loads and its tail is
+            // light; "zip" (default) alternating costliest and cheapest, which spreads the VALU
+            // work evenly over the stream (the packed vocabulary puts the widely shared words --
+            // 120-250 VALU per quad -- at the end, the rare ones at 4-40 first): -5.5% config 2
+            // vs memory order; "snake" equal VALU per burst
+            const char* qo = getenv("DICE_PROG_QORDER");
+            const std::string mode = qo && *qo ? qo : "zip";
+            std::vector<size_t> idx(quads.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+            if (mode == "desc" || mode == "zip")
+                std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
+            if (mode == "zip") {
+                std::vector<size_t> z;
+                for (size_t lo = 0, hi = idx.size(); lo < hi;) {
+                    z.push_back(idx[lo++]);
+                    if (lo < hi) z.push_back(idx[--hi]);
+                }
+                idx.swap(z);
+            }
+            if (mode == "snake") {   // equal VALU per burst: costliest-first dealt over bursts in snake order
+                const char* b_env2 = getenv("DICE_PROG_BURST");
+                const size_t nb2 = (size_t)std::max(1, b_env2 && *b_env2 ? atoi(b_env2) : 5);
+                const size_t ng2 = (idx.size() + nb2 - 1) / nb2;
+                std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
+                std::vector<std::vector<size_t>> bursts(ng2);
+                size_t k = 0;
+                for (size_t i = 0; i < idx.size(); ++i) {
+                    // snake over bursts that still have room
+                    for (;;) {
+                        const size_t round = k / ng2, pos = k % ng2;
+                        const size_t bi = (round % 2 == 0) ? pos : ng2 - 1 - pos;
+                        ++k;
+                        if (bursts[bi].size() < nb2) {
+                            bursts[bi].push_back(idx[i]);
+                            break;
+                        }
+                    }
+                }
+                idx.clear();
+                for (auto& b : bursts) idx.insert(idx.end(), b.begin(), b.end());
+            }
+            std::vector<int32_t> q2;
+            std::vector<std::pair<size_t, size_t>> r2;
+            for (size_t i : idx) {
+                q2.push_back(quads[i]);
+                r2.push_back(range[i]);
+            }
+            quads.swap(q2);
+            range.swap(r2);
+        }
         const char* sched_env = getenv("DICE_PROG_SCHED");
         const bool ring = sched_env && strcmp(sched_env, "ring") == 0;
         if (ring) {
@@ -424,14 +477,13 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             pd = std::max(1, std::min<int>(pd, (int)quads.size()));
             for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
             prologue << "__builtin_amdgcn_sched_barrier(0);\n";
-            size_t e = 0;
             for (size_t qi = 0; qi < quads.size(); ++qi) {
                 const int slot = (int)(qi % pd);
                 prologue << "{ const uint4 v = pf" << slot << ";";
                 if (qi + pd < quads.size())
                     prologue << " pf" << slot << " = ldq(fp + " << quads[qi + pd] * 64 << "); __builtin_amdgcn_sched_barrier(0);";
                 prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                prologue << acc_quad(dm, e, quads[qi]);
+                prologue << acc_quad(dm, range[qi].first, range[qi].second, quads[qi]);
                 prologue << "}\n";
             }
         } else {
@@ -450,7 +502,6 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
                 o << "\n";
             };
             auto stream = [&](std::ostringstream& o) {
-                size_t e = 0;
                 for (size_t g = 0; g < ng; ++g) {
                     const int cur = (int)(g % 2), nxt = 1 - cur;
                     o << "__builtin_amdgcn_sched_barrier(0);\n";
@@ -458,7 +509,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
                     o << "__builtin_amdgcn_sched_barrier(0);\n";
                     for (size_t i = g * nb; i < std::min(quads.size(), (g + 1) * nb); ++i) {
                         o << "{ const uint4 v = p" << cur << "_" << (i - g * nb) << "; const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                        o << acc_quad(dm, e, quads[i]);
+                        o << acc_quad(dm, range[i].first, range[i].second, quads[i]);
                         o << "}\n";
                     }
                 }

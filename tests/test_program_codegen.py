@@ -72,16 +72,21 @@ def run_host(corpus, fb, k, tmp_path):
 
 
 SCHEDULES = {
-    'burst3': {},                                    # default: bursts of 3 quads, non-temporal loads
+    'burst3': {'DICE_PROG_BURST': '3'},
     'burst7': {'DICE_PROG_BURST': '7', 'DICE_PROG_NT': '0'},
     'ring8': {'DICE_PROG_SCHED': 'ring'},
+    'burst5desc': {'DICE_PROG_QORDER': 'desc'},
+    'burst4zip': {'DICE_PROG_QORDER': 'zip', 'DICE_PROG_BURST': '4'},
+    'burst5snake': {'DICE_PROG_QORDER': 'snake'},
+    'burst5asc': {'DICE_PROG_QORDER': 'asc'},
 }
 
 
 @pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
-@pytest.mark.parametrize('k,sched', [(3, 'burst3'), (5, 'burst7'), (5, 'ring8')])
+@pytest.mark.parametrize('k,sched', [(3, 'burst3'), (5, 'burst7'), (5, 'ring8'), (3, 'burst5desc'), (5, 'burst4zip'),
+                                      (3, 'burst5snake'), (5, 'burst5asc')])
 def test_generated_program_matches_oracle(tmp_path, monkeypatch, k, sched):
-    for key in ('DICE_PROG_SCHED', 'DICE_PROG_BURST', 'DICE_PROG_NT'):
+    for key in ('DICE_PROG_SCHED', 'DICE_PROG_BURST', 'DICE_PROG_NT', 'DICE_PROG_QORDER'):
         monkeypatch.delenv(key, raising=False)
     for key, v in SCHEDULES[sched].items():
         monkeypatch.setenv(key, v)
