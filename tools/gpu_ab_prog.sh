@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of the quad processing order (memory order vs costliest-first vs zipped) on config 2.
+# A/B of quad orders x burst sizes on config 2 (interleaved, one box).
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
 run() {
@@ -8,8 +8,9 @@ run() {
   python -c "import json;d=json.load(open('gpurun_out/ab/$tag.json'));print('$tag', round(d['roofline']['launch_ms']*1000,1), 'us')"
 }
 for rep in 1 2 3; do
-run asc_$rep DICE_X=0
-run desc_$rep DICE_PROG_QORDER=desc
-run zip_$rep DICE_PROG_QORDER=zip
-run desc4_$rep DICE_PROG_QORDER=desc DICE_PROG_BURST=4
+run zip5_$rep DICE_X=0
+run snake5_$rep DICE_PROG_QORDER=snake
+run zip4_$rep DICE_PROG_BURST=4
+run zip6_$rep DICE_PROG_BURST=6
+run snake4_$rep DICE_PROG_QORDER=snake DICE_PROG_BURST=4
 done
