@@ -530,7 +530,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
     if (diag && strcmp(diag, "noepi") == 0) {
         std::ostringstream mb;
-        mb << "bi = 0; bd = 1; bo = 0; _Pragma(\"unroll\") for (int i = 0; i < NT; ++i) bo += acc[i];\n";
+        mb << "bd = 1; bo = 0; _Pragma(\"unroll\") for (int i = 0; i < NT; ++i) bo += acc[i];\n";
         match_body.str(mb.str());
     }
     emit_macro(s, "MATCH_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", match_body.str() + "}");

@@ -4,17 +4,13 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/diag
 run() {
   local tag=$1; shift
-  env "$@" timeout -k 10 200 python bench.py --steps 50 --warmup 5 --no-cpu-baseline "${EXTRA[@]}" > gpurun_out/diag/$tag.json 2> gpurun_out/diag/$tag.err || { echo "$tag failed"; tail -5 gpurun_out/diag/$tag.err; exit 1; }
+  env "$@" timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline "${EXTRA[@]}" > gpurun_out/diag/$tag.json 2> gpurun_out/diag/$tag.err || { echo "$tag failed"; tail -5 gpurun_out/diag/$tag.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/diag/$tag.json'));print('$tag', round(d['roofline']['launch_ms']*1000,1), 'us')"
 }
 for rep in 1 2; do
 EXTRA=(--probe); run probe_$rep DICE_X=0
 EXTRA=()
-run ring_$rep DICE_PROG_SCHED=ring
-run ring_noacc_$rep DICE_PROG_SCHED=ring DICE_PROG_DIAG=noacc
-run ring_noepi_$rep DICE_PROG_SCHED=ring DICE_PROG_DIAG=noepi
-run b4_$rep DICE_PROG_TILES=1
-run b4_noacc_$rep DICE_PROG_TILES=1 DICE_PROG_DIAG=noacc
-run b4_noepi_$rep DICE_PROG_TILES=1 DICE_PROG_DIAG=noepi
-run b4x2_noepi_$rep DICE_PROG_TILES=2 DICE_PROG_DIAG=noepi
+run full_$rep DICE_X=0
+run noacc_$rep DICE_PROG_DIAG=noacc
+run noepi_$rep DICE_PROG_DIAG=noepi
 done
