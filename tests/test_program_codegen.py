@@ -112,3 +112,34 @@ def test_generated_program_matches_oracle(tmp_path, monkeypatch, k, sched):
         ranked = O.matches_by_similarity(otpl, f.oracle, cc_fp=f.cc)[:k]
         assert tki[i].tolist() == [r[0] for r in ranked] + [-1] * (k - len(ranked)), i
         assert tks[i, :len(ranked)].tolist() == [r[1] for r in ranked], i
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+@pytest.mark.parametrize('epi', ['stream', 'tail'])
+def test_exact_ties_later_key_wins(tmp_path, monkeypatch, epi):
+    """Corpus with byte-identical templates under later keys: every file ties between a template
+    and its clone, and the clone (later in key order) must rank first (dice.rb:39, stable sort +
+    reverse) -- whether the epilogues run inside the stream (order-independent ranking) or after."""
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from oracle.native import OracleScorer
+    for key in ('DICE_PROG_SCHED', 'DICE_PROG_BURST', 'DICE_PROG_NT', 'DICE_PROG_QORDER', 'DICE_PROG_EPI'):
+        monkeypatch.delenv(key, raising=False)
+    if epi == 'tail':
+        monkeypatch.setenv('DICE_PROG_EPI', 'tail')
+    base = [License.find(k) for k in ('apache-2.0', 'bsd-2-clause', 'isc', 'mit', 'mpl-2.0', 'unlicense')]
+    clones = [License('zz-' + l.key, {'title': l.title}, content_normalized=l.content_normalized(),
+                      alt_segments=l.spdx_alt_segments()) for l in base]
+    templates = sorted(base + clones, key=lambda l: l.key)
+    corpus = TemplateCorpus(templates)
+    files = make_files(templates, 300, 5) + [NormFile('')]
+    fb = corpus.intern_files(files)
+    best, ov, score, mov, msc, tki, tks = run_host(corpus, fb, 3, tmp_path)
+    orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                       corpus.length, corpus.is_cc, corpus.n_vocab)
+    eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0)
+    assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+    keys = [t.key for t in templates]
+    matched = best[best >= 0]
+    assert len(matched) > 50 and all(keys[b].startswith('zz-') for b in matched)
+    assert all(keys[i].startswith('zz-') for i in tki[:, 0] if i >= 0)
