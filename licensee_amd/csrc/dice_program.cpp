@@ -106,23 +106,6 @@ __device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
     }
     return sc(oa & 0xFFFFFFu, da) >= sc(ob & 0xFFFFFFu, db);
 }
-// Match-kernel ranking, independent of the order templates are offered in: candidate a (template
-// index + 1 in bits 24-31, overlap below) beats the running best bo when its score is higher, or
-// equal and its key later (stable ascending sort + reverse, dice.rb:39). bo == 0: none yet.
-template <bool FAST>
-__device__ __forceinline__ bool win(u32 a, i32 d, u32 bo, i32 bd) {
-    if (FAST) {
-#if NARROW_MUL
-        const u32 p1 = mul24(a, (u32)bd), p2 = mul24(bo, (u32)d);
-#else
-        const u64 p1 = (u64)(a & 0xFFFFFFu) * (u64)(u32)bd, p2 = (u64)(bo & 0xFFFFFFu) * (u64)(u32)d;
-#endif
-        return p1 > p2 || (p1 == p2 && a > bo);
-    }
-    if (bo == 0u) return true;
-    const double sa = sc(a & 0xFFFFFFu, d), sb = sc(bo & 0xFFFFFFu, bd);
-    return sa > sb || (sa == sb && a > bo);
-}
 #define ACC(d, m) a = __builtin_popcount(f[d] & (m##u)) + a
 #define ACCF(d) a = __builtin_popcount(f[d]) + a
 )HIP";
@@ -140,16 +123,17 @@ extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
     const u32 wf = wfp[file];
     const i32 lf = lenp[file];
     const bool cc = ccp[file] != 0;
+    FILE_PROLOGUE
     const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
-    // running best: bo = (template index + 1) << 24 | overlap (0: none yet), bd = its denominator
-    u32 bo = 0u; i32 bd = 1;
+    // running best: bo = template index << 24 | overlap (0xFF: none yet), bd = its denominator
+    u32 bo = 0xFF000000u; i32 bd = 1;
     if (__all(fast)) {
-        MATCH_STREAM(true)
+        MATCH_BODY(true)
     } else {
-        MATCH_STREAM(false)
+        MATCH_BODY(false)
     }
     if (file < n) {
-        const i32 bi = (i32)(bo >> 24) - 1;
+        const i32 bi = (bo >> 24) == 0xFFu ? -1 : (i32)(bo >> 24);
         const u32 bov = bo & 0xFFFFFFu;
         const double s = bi >= 0 ? sc(bov, bd) : 0.0;
         best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
@@ -392,13 +376,12 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     auto offer = [&](int32_t i) {
         std::ostringstream o;
         if (t->is_cc[i]) o << "if (!cc) ";
-        // a carries the template index + 1 in its top byte (ACC_INIT): one select moves index and
+        // a carries the template index in its top byte (ACC_INIT): one select moves index and
         // overlap together; v_mul_u32_u24 reads only the low 24 bits (the overlap)
-        o << "{ if (win<FASTV>(a, d, bo, bd)) { bo = a; bd = d; } }";
+        o << "{ if ((!FASTV && (bo >> 24) == 0xFFu) || ge<FASTV>(a, d, bo, bd)) { bo = a; bd = d; } }";
         return o.str();
     };
     std::ostringstream match_body, matrix_body, prologue;
-    std::string match_stream;   // match kernel: the file stream with its epilogues (MATCH_STREAM)
     if (order == 't') {
         prologue << "u32 f[WQ * 4];\n_Pragma(\"unroll\") for (int q = 0; q < WQ; ++q) { const uint4 v = fp[q * 64]; "
                     "f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w; }\n";
@@ -536,40 +519,6 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             prologue << decl.str();
             group_loads(prologue, 0, 0);
             stream(prologue);
-            // Match kernel: each template's epilogue (denominator, rank, select) right after the last
-            // quad it has entries in, so most of that VALU work overlaps the loads still in flight
-            // instead of running after the stream (the ranking is order-independent, see win()).
-            const char* ep_env = getenv("DICE_PROG_EPI");   // "tail": all epilogues after the stream
-            if (!(ep_env && strcmp(ep_env, "tail") == 0)) {
-                std::vector<int> last(t->n_templates, -1);
-                for (size_t i = 0; i < quads.size(); ++i)
-                    for (size_t e = range[i].first; e < range[i].second; ++e)
-                        last[dm[e].tpl] = std::max(last[dm[e].tpl], (int)i);
-                auto epi = [&](std::ostringstream& o, int pos) {
-                    for (int32_t ti = 0; ti < t->n_templates; ++ti)
-                        if (last[ti] == pos)
-                            o << "{ const u32 a = acc[" << ti << "]; i32 d; " << den[ti] << offer(ti) << " }\n";
-                };
-                std::ostringstream ms;
-                ms << "u32 acc[NT];\n_Pragma(\"unroll\") for (int i = 0; i < NT; ++i) acc[i] = ACC_INIT(i);\n"
-                   << decl.str();
-                group_loads(ms, 0, 0);
-                epi(ms, -1);   // templates without entries
-                for (size_t g = 0; g < ng; ++g) {
-                    const int cur = (int)(g % 2), nxt = 1 - cur;
-                    ms << "__builtin_amdgcn_sched_barrier(0);\n";
-                    if (g + 1 < ng) group_loads(ms, g + 1, nxt);
-                    ms << "__builtin_amdgcn_sched_barrier(0);\n";
-                    for (size_t i = g * nb; i < std::min(quads.size(), (g + 1) * nb); ++i) {
-                        ms << "{ const uint4 v = p" << cur << "_" << (i - g * nb)
-                           << "; const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                        ms << acc_quad(dm, range[i].first, range[i].second, quads[i]);
-                        ms << "}\n";
-                        epi(ms, (int)i);
-                    }
-                }
-                match_stream = ms.str();
-            }
         }
         for (int32_t i = 0; i < t->n_templates; ++i) {
             match_body << "{ const u32 a = acc[" << i << "]; i32 d; " << den[i] << offer(i) << " }\n";
@@ -584,10 +533,8 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
         mb << "bd = 1; bo = 0; _Pragma(\"unroll\") for (int i = 0; i < NT; ++i) bo += acc[i];\n";
         match_body.str(mb.str());
     }
-    if (match_stream.empty() || (diag && strcmp(diag, "noepi") == 0))
-        match_stream = prologue.str() + match_body.str();   // stream, then every epilogue in key order
-    emit_macro(s, "MATCH_STREAM(FASTV_) { constexpr bool FASTV = FASTV_;", match_stream + "}");
-    s << "#define ACC_INIT(i) (((u32)(i) + 1u) << 24)\n" << kMatchKernel << "#undef ACC_INIT\n#define ACC_INIT(i) 0u\n";
+    emit_macro(s, "MATCH_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", match_body.str() + "}");
+    s << "#define ACC_INIT(i) ((u32)(i) << 24)\n" << kMatchKernel << "#undef ACC_INIT\n#define ACC_INIT(i) 0u\n";
     s << kMatrixOffer;
     emit_macro(s, "MATRIX_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", matrix_body.str() + "}");
     for (int km : {4, 16}) {
