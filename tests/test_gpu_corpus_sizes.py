@@ -67,3 +67,29 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
         assert np.array_equal(tks[valid], np.take_along_axis(emsc, order, 1)[valid])
     finally:
         sc.close()
+
+
+@pytest.mark.parametrize('n_files', [0, 1, 63, 150, 1000])
+def test_lds_ragged_batches(n_files, monkeypatch):
+    """LDS kernel (T = 130) on batches that end mid-tile and mid-group: a workgroup holds 2 tiles of 64
+    files, so 150 files leave an odd tile count and a 22-file tail; 0 files launch nothing."""
+    from licensee_amd._native import FileBatch, Scorer
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    from oracle.native import OracleScorer
+    monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
+    c = TemplateCorpus(corpus_of(130))
+    fb = SyntheticCorpus(c).generate(0, max(n_files, 1), seed=7, nthreads=8)
+    fb = FileBatch(fb.bits[:n_files], fb.wordset_size[:n_files], fb.length[:n_files], fb.cc_false_positive[:n_files])
+    sc = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab, device=0)
+    try:
+        assert sc.info()[2] == KIND['lds']
+        orc = OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
+        best, ov, score = sc.match(fb, 98.0)
+        assert best.shape == ov.shape == score.shape == (n_files,)
+        if n_files == 0:
+            return
+        eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=8)
+        assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+    finally:
+        sc.close()

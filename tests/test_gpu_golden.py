@@ -176,7 +176,7 @@ def test_full_size_matrix_consistency(big):
     assert not np.isin(tki[flagged], cc_t).any()
 
 
-@pytest.mark.parametrize('kernel', ['lds', 'dense'])
+@pytest.mark.parametrize('kernel', ['lds', 'lds-g12', 'lds-g24', 'dense'])
 def test_large_corpus_600_templates(kernel, monkeypatch):
     from licensee_amd._native import Scorer
     from licensee_amd.corpus import TemplateCorpus
@@ -190,9 +190,11 @@ def test_large_corpus_600_templates(kernel, monkeypatch):
         monkeypatch.setenv('DICE_FORCE_DENSE', '1')
     else:
         monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
+    # templates per wave per pass of the LDS kernel: 16 (default, 3 passes here), 12 (4), 24 (2)
+    monkeypatch.setenv('DICE_LDS_G', kernel[5:] if kernel.startswith('lds-g') else '16')
     sc = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
                 corpus.is_cc, corpus.n_vocab, device=0)
-    assert sc.info()[2] == {'lds': 2, 'dense': 0}[kernel]
+    assert sc.info()[2] == (0 if kernel == 'dense' else 2)
     orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
                        corpus.length, corpus.is_cc, corpus.n_vocab)
     best, ov, score = sc.match(fb, 98.0)
