@@ -119,7 +119,7 @@ template <int G>
 __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
     const uint4* __restrict__ tiles, int64_t n, int32_t wq, int32_t nslab, int32_t T,
     const int32_t* __restrict__ rec, const uint4* __restrict__ ep, const int32_t* __restrict__ wave_t0,
-    int32_t npass, const int4* __restrict__ tc, const uint32_t* __restrict__ wfp,
+    int32_t npass, int32_t snake, const int4* __restrict__ tc, const uint32_t* __restrict__ wfp,
     const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
     int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out) {
     // one LDS object: the rings in the low 32 KiB (LDS-DMA addresses them through M0), the
@@ -158,25 +158,31 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
 #pragma unroll
             for (int f = 0; f < kTiles; ++f) acc[j][f] = 0;
 
-        for (int s = 0; s < nslab; ++s) {
-            // stage slab s: rows r = wave + 16 i of (tile f = r / 64, quad q = r % 64); one
-            // 1 KiB coalesced load per row, two ds_write_b64 per lane
-            uint4 stage[kTiles * kSlabQuads / kLdsWaves];
+        for (int si = 0; si < nslab; ++si) {
+            // snake order: odd passes walk the slabs backwards, so a pass starts on the slab the
+            // previous one ended on, which is still in LDS (npass - 1 fewer stagings)
+            const int s = (snake && (pass & 1)) ? nslab - 1 - si : si;
+            const bool restage = !(snake && pass > 0 && si == 0);
+            if (restage) {
+                // stage slab s: rows r = wave + 16 i of (tile f = r / 64, quad q = r % 64); one
+                // 1 KiB coalesced load per row, two ds_write_b64 per lane
+                uint4 stage[kTiles * kSlabQuads / kLdsWaves];
 #pragma unroll
-            for (int i = 0; i < kTiles * kSlabQuads / kLdsWaves; ++i) {
-                const int r = wave + i * kLdsWaves;
-                const int f = r / kSlabQuads, q = r % kSlabQuads;
-                const int qg = s * kSlabQuads + q;
-                const bool ok = tile0 + f < n_tiles && qg < wq;
-                stage[i] = ok ? tiles[((tile0 + f) * wq + qg) * kWave + lane] : make_uint4(0, 0, 0, 0);
-            }
-            __syncthreads();   // the previous slab's readers are done
+                for (int i = 0; i < kTiles * kSlabQuads / kLdsWaves; ++i) {
+                    const int r = wave + i * kLdsWaves;
+                    const int f = r / kSlabQuads, q = r % kSlabQuads;
+                    const int qg = s * kSlabQuads + q;
+                    const bool ok = tile0 + f < n_tiles && qg < wq;
+                    stage[i] = ok ? tiles[((tile0 + f) * wq + qg) * kWave + lane] : make_uint4(0, 0, 0, 0);
+                }
+                __syncthreads();   // the previous slab's readers are done
 #pragma unroll
-            for (int i = 0; i < kTiles * kSlabQuads / kLdsWaves; ++i) {
-                const int r = wave + i * kLdsWaves;
-                const int f = r / kSlabQuads, q = r % kSlabQuads;
-                slab[((2 * q) * kTiles + f) * kWave + lane] = make_uint2(stage[i].x, stage[i].y);
-                slab[((2 * q + 1) * kTiles + f) * kWave + lane] = make_uint2(stage[i].z, stage[i].w);
+                for (int i = 0; i < kTiles * kSlabQuads / kLdsWaves; ++i) {
+                    const int r = wave + i * kLdsWaves;
+                    const int f = r / kSlabQuads, q = r % kSlabQuads;
+                    slab[((2 * q) * kTiles + f) * kWave + lane] = make_uint2(stage[i].x, stage[i].y);
+                    slab[((2 * q + 1) * kTiles + f) * kWave + lane] = make_uint2(stage[i].z, stage[i].w);
+                }
             }
             // this wave's record stream for slab s: runs of templates [tb, te), contiguous; the
             // first two 64-record chunks go to the ring now
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
             const int32_t nchunk = (total + 63) / 64;
             if (nchunk > 0) __builtin_amdgcn_global_load_lds(src + lane, &ring[wave][0], 16, 0, 0);
             if (nchunk > 1) __builtin_amdgcn_global_load_lds(src + 64 + lane, &ring[wave][64], 16, 0, 0);
-            __syncthreads();   // slab writes visible to every wave
+            if (restage) __syncthreads();   // slab writes visible to every wave
 
             int32_t p = 0;     // stream position (records), a multiple of 4
 #pragma unroll
@@ -338,6 +344,8 @@ int lds_setup(dice_ctx* c, const dice_templates* t) {
     c->lds_npass = npass;
     c->lds_entries = (int64_t)ep.size() - kRingPad;
     c->lds_g = G;
+    const char* sn = getenv("DICE_LDS_SNAKE");   // A/B knob: 0 = every pass walks slabs 0..nslab-1
+    c->lds_snake = !(sn && *sn == '0');
     c->kind = 2;
     return DICE_OK;
 }
@@ -348,7 +356,7 @@ static void launch(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t groups = (n_tiles + kTiles - 1) / kTiles;
     hipLaunchKernelGGL((dice_lds_match<G>), dim3((unsigned)groups), dim3(kLdsWaves * kWave), 0, s, b->d_tiles, b->n,
                        c->wq, c->lds_nslab, c->T, (const int32_t*)c->d_lrec, (const uint4*)c->d_lep,
-                       (const int32_t*)c->d_lwt, c->lds_npass, c->d_tc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
+                       (const int32_t*)c->d_lwt, c->lds_npass, c->lds_snake, c->d_tc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
                        b->d_ov, b->d_score);
 }
 
