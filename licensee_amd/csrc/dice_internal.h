@@ -49,7 +49,7 @@ struct dice_ctx {
     void* d_lep = nullptr;
     void* d_les = nullptr;
     void* d_lwt = nullptr;
-    int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1;
+    int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1, lds_wide = 0, lds_tiles = 2;
     int64_t lds_entries = 0;
 };
 
