@@ -69,10 +69,14 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
         sc.close()
 
 
+@pytest.mark.parametrize('tiles', [2, 4])
 @pytest.mark.parametrize('n_files', [0, 1, 63, 150, 1000])
-def test_lds_ragged_batches(n_files, monkeypatch):
-    """LDS kernel (T = 130) on batches that end mid-tile and mid-group: a workgroup holds 2 tiles of 64
-    files, so 150 files leave an odd tile count and a 22-file tail; 0 files launch nothing."""
+def test_lds_ragged_batches(n_files, tiles, monkeypatch):
+    """LDS kernel (T = 130) on batches that end mid-tile and mid-group: a workgroup holds 2 (or, as
+    the DICE_LDS_TILES=4 A/B layout, 4) tiles of 64 files, so 150 files leave a partial group and a
+    22-file tail; 0 files launch nothing."""
+    monkeypatch.setenv('DICE_LDS_TILES', str(tiles))
+    monkeypatch.setenv('DICE_LDS_G', '16' if tiles == 2 else '12')
     from licensee_amd._native import FileBatch, Scorer
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
