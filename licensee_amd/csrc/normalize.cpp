@@ -70,7 +70,7 @@ bool python_only(char32_t c) { return c == 0x130 || c == 0x131 || c == 0x17F || 
 struct Ctx {
     std::map<std::string, Regex> re;
     std::vector<std::pair<Str, Str>> spell;
-    std::vector<int> spell_first[128];   // spell indices by first character, union order kept
+    std::vector<int> spell_first2[128 * 128];   // spell indices by first two characters, union order kept
     // Unicode tables (lh_set_unicode): Python str.lower() of non-ASCII code points
     bool unicode = false;
     std::unordered_map<char32_t, char32_t> lower;
@@ -171,10 +171,10 @@ struct Normalizer {
                     ++i;
                     continue;
                 }
-                if (ch < 128)
-                    for (int si : c.spell_first[ch]) {
+                if (ch < 128 && i + 1 < n && cur[i + 1] < 128)
+                    for (int si : c.spell_first2[ch * 128 + cur[i + 1]]) {
                         const Str& k = c.spell[si].first;
-                        if (k.size() <= n - i && cur[i + 1] == k[1] && cur.compare(i, k.size(), k) == 0 &&
+                        if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 &&
                             (i + k.size() == n || !word(cur[i + k.size()]))) {
                             at = i;
                             klen = k.size();
@@ -225,7 +225,8 @@ struct Normalizer {
         strip_re(c.R("hrs"));
         strip_comments();
         strip_re(c.R("markdown_headings"));
-        sub_re(c.R("link_markup"), U"\\1");
+        // \[(.+?)\]\(.+?\) needs a literal "](": without one the lazy scans from every '[' are wasted
+        if (contains(cur, "](")) sub_re(c.R("link_markup"), U"\\1");
         strip_title();
         strip_re(c.R("version"));
         for (auto& ch : cur) {
@@ -369,8 +370,9 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
         for (int32_t i = 0; i < n_spell; ++i) {
             c->spell.push_back({rx::from_utf8(spell_from[i]), rx::from_utf8(spell_to[i])});
             const Str& k = c->spell.back().first;
-            if (k.size() < 2 || k[0] >= 128) throw std::runtime_error("spelling keys: >= 2 characters, ASCII first");
-            c->spell_first[k[0]].push_back(i);
+            if (k.size() < 2 || k[0] >= 128 || k[1] >= 128)
+                throw std::runtime_error("spelling keys: >= 2 characters, ASCII first two");
+            c->spell_first2[k[0] * 128 + k[1]].push_back(i);
         }
         for (int32_t i = 0; i < n_vocab; ++i) c->vocab.emplace(vocab[i], i);
         c->n_vocab = n_vocab;

@@ -118,6 +118,32 @@ def test_fuzz_texts(hp):
     assert checked > 350 and fell > 0
 
 
+def test_spelling_and_link_markup_fuzz(hp):
+    """normalize_spelling (content_helper.rb:314-316) and strip_link_markup (:289-291) on texts
+    dense in varietal words: alone, recased, prefixed/suffixed, split, bracketed, inside link
+    markup, beside punctuation/dashes/quotes/non-ASCII -- exercises the native two-character key
+    index and the "](" gate of the link pass."""
+    from licensee_amd.content_helper import VARIETAL_WORDS
+    rng = random.Random(3)
+    keys = list(VARIETAL_WORDS)
+    checked = 0
+    for i in range(300):
+        words = []
+        for _ in range(rng.randint(1, 60)):
+            k = rng.choice(keys)
+            words.append(rng.choice([k, k.upper(), k.capitalize(), k + 's', 'x' + k, k + '_', k + '-', '(' + k + ')',
+                                     k[:2], k[:3] + ' ' + k[3:], '[' + k + '](http://a)', '[' + k + ']']))
+            if rng.random() < 0.3:
+                words.append(rng.choice(['&', '--', '\u2014', '"q"', '\n', '  ', '\u00e9', 'colour', 'licence', '](']))
+        text = ' '.join(words)
+        got = hp.normalize(text, 'LICENSE')
+        if got is None:
+            continue
+        checked += 1
+        assert got == LicenseFile(text, 'LICENSE').content_normalized(), (i, text[:200])
+    assert checked > 250
+
+
 def test_batch_prep_matches_python(hp):
     from licensee_amd.matchers import Copyright, Exact
     vend = golden('vendored.json')['templates']
