@@ -215,7 +215,13 @@ struct Normalizer {
             }
         }
         cur.resize(w);
-        squeeze_strip();
+        // no ' ' runs are left, so squeeze(' ') is the identity: strip only
+        size_t b = cur.size();
+        while (b > 0 && is_strip_char(cur[b - 1])) --b;
+        cur.resize(b);
+        size_t a = 0;
+        while (a < cur.size() && is_strip_char(cur[a])) ++a;
+        if (a) cur.erase(0, a);
         clean = true;
     }
 
