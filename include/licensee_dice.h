@@ -118,10 +118,13 @@ int dice_batch_match(dice_batch *batch, double threshold, void *stream);
 /* Device-resident matrix results are template-major ([T][n] overlap/score, [k][n] top-k) so
  * every store is coalesced; dice_batch_download_matrix returns them row-major. */
 int dice_batch_matrix(dice_batch *batch, int32_t k, void *stream);
-/* D2H of results (synchronizes `stream`); NULL outputs are skipped. */
+/* D2H of results (synchronizes `stream`); NULL outputs are skipped.
+ * dice_batch_download_matrix: overlap/score are [n][T]; topk_index/topk_score are [n][k] and
+ * `k` must equal the k of the last dice_batch_matrix call on this batch (DICE_E_ARG
+ * otherwise, so a caller's buffer is never written past its [n][k] extent). */
 int dice_batch_download_match(dice_batch *batch, int32_t *best, uint32_t *overlap,
                               double *score, void *stream);
-int dice_batch_download_matrix(dice_batch *batch, uint32_t *overlap, double *score,
+int dice_batch_download_matrix(dice_batch *batch, uint32_t *overlap, double *score, int32_t k,
                                int32_t *topk_index, double *topk_score, void *stream);
 /* Device pointers of the match results (int32 best, uint32 overlap, double score). */
 int dice_batch_result_ptrs(dice_batch *batch, void **best, void **overlap, void **score);

@@ -69,7 +69,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_match': (ctypes.c_int, [vp, ctypes.c_double, vp]),
         'dice_batch_matrix': (ctypes.c_int, [vp, i32, vp]),
         'dice_batch_download_match': (ctypes.c_int, [vp, vp, vp, vp, vp]),
-        'dice_batch_download_matrix': (ctypes.c_int, [vp, vp, vp, vp, vp, vp]),
+        'dice_batch_download_matrix': (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
         'dice_batch_result_ptrs': (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         'dice_batch_bytes_per_file': (i64, [vp]),
         'dice_batch_stream_probe': (ctypes.c_int, [vp, vp]),
@@ -220,6 +220,7 @@ class DeviceBatch:
 
     def matrix(self, k: int, stream: int = 0):
         _check(load_library().dice_batch_matrix(self._b, int(k), stream or None))
+        self.k = int(k)
 
     def download_match(self, stream: int = 0):
         n = self.n
@@ -229,16 +230,19 @@ class DeviceBatch:
         _check(load_library().dice_batch_download_match(self._b, _ptr(best), _ptr(ov), _ptr(score), stream or None))
         return best, ov, score
 
-    def download_matrix(self, k: int, stream: int = 0):
+    def download_matrix(self, k: Optional[int] = None, stream: int = 0):
+        """Matrix results of the last :meth:`matrix` call; the top-k arrays are [n][k] with
+        that call's k (a different ``k`` raises, as the C-ABI returns DICE_E_ARG)."""
         n, T = self.n, self.scorer.n_templates
+        k = getattr(self, 'k', 0) if k is None else int(k)
         ov = np.empty((n, T), np.uint32)
         score = np.empty((n, T), np.float64)
-        tki = np.empty((n, max(k, 1)), np.int32)
-        tks = np.empty((n, max(k, 1)), np.float64)
-        _check(load_library().dice_batch_download_matrix(self._b, _ptr(ov), _ptr(score),
+        tki = np.empty((n, k), np.int32)
+        tks = np.empty((n, k), np.float64)
+        _check(load_library().dice_batch_download_matrix(self._b, _ptr(ov), _ptr(score), k,
                                                          _ptr(tki) if k else None, _ptr(tks) if k else None,
                                                          stream or None))
-        return ov, score, tki[:, :k], tks[:, :k]
+        return ov, score, tki, tks
 
     def result_ptrs(self):
         p = [ctypes.c_void_p() for _ in range(3)]

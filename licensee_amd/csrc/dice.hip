@@ -554,9 +554,12 @@ int dice_batch_download_match(dice_batch* b, int32_t* best, uint32_t* ov, double
     return DICE_OK;
 }
 
-int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32_t* tki, double* tks,
+int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32_t k, int32_t* tki, double* tks,
                                void* stream) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
+    if ((tki || tks) && k != b->k_used)
+        return fail(DICE_E_ARG, "top-k buffers are [n][k]: k must equal the last dice_batch_matrix k (" +
+                                    std::to_string(b->k_used) + ")");
     dice_ctx* c = b->ctx;
     DeviceGuard g(c->device);
     hipStream_t s = pick_stream(c, stream);
@@ -631,7 +634,7 @@ int dice_similarity_matrix(dice_ctx* ctx, const dice_files* f, uint32_t* ov, dou
     if (rc) return rc;
     if ((rc = dice_batch_upload(b, f, nullptr))) return rc;
     if ((rc = dice_batch_matrix(b, k, nullptr))) return rc;
-    return dice_batch_download_matrix(b, ov, score, k > 0 ? tki : nullptr, k > 0 ? tks : nullptr, nullptr);
+    return dice_batch_download_matrix(b, ov, score, k, k > 0 ? tki : nullptr, k > 0 ? tks : nullptr, nullptr);
 }
 
 }  // extern "C"

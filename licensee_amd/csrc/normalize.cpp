@@ -9,8 +9,11 @@
 // time and run on rx (rx.h), so both host paths share a single pattern source.
 // Texts containing characters whose Python case mapping or \b / \w semantics could differ
 // from the ASCII rules implemented here (non-ASCII letters/digits) -- and HTML files -- are
-// reported as status 1 and normalized by the Python path instead.
+// reported as status 1 and normalized by the Python path instead, as are texts whose match
+// would nest deeper than the regex engine's frame limit (rx::TooDeep; e.g. thousands of
+// consecutive copyright lines under the copyright pattern's repeated group).
 #include <malloc.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -332,7 +335,50 @@ struct FileOut {
     bool cc = false, copyright = false;
 };
 
+void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o);
+
+// prep_one with the regex engine's depth abort mapped to "use the Python path"
 void prep_one(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o) {
+    try {
+        prep_one_impl(c, data, len, filename, is_file, o);
+    } catch (const rx::TooDeep&) {
+        o = FileOut();
+        o.status = 1;
+    }
+}
+
+// Batch workers run on threads with kWorkerStack bytes of stack (reserved virtual memory; only
+// touched pages are committed) and a matching regex frame limit (~0.27 KiB per frame).
+constexpr size_t kWorkerStack = size_t(256) << 20;
+constexpr size_t kWorkerMatchDepth = 600000;
+
+template <class F>
+void run_workers(int32_t nthreads, F& work) {
+    struct Arg {
+        F* fn;
+    } arg{&work};
+    auto entry = [](void* p) -> void* {
+        rx::set_match_depth(kWorkerMatchDepth);
+        (*static_cast<Arg*>(p)->fn)();
+        return nullptr;
+    };
+    std::vector<pthread_t> th;
+    pthread_attr_t attr;
+    pthread_attr_init(&attr);
+    pthread_attr_setstacksize(&attr, kWorkerStack);
+    for (int32_t t = 0; t < nthreads; ++t) {
+        pthread_t id;
+        if (pthread_create(&id, &attr, entry, &arg) == 0) th.push_back(id);
+    }
+    pthread_attr_destroy(&attr);
+    if (th.empty()) {   // no thread could be created: run here (default frame limit)
+        work();
+        return;
+    }
+    for (auto& id : th) pthread_join(id, nullptr);
+}
+
+void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o) {
     Str content = rx::from_utf8(std::string(data, (size_t)len));
     if (is_file) {   // universal newline (project_file.rb:41)
         Str t;
@@ -494,9 +540,7 @@ int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t
             }
         }
     };
-    std::vector<std::thread> th;
-    for (int32_t t = 0; t < nthreads; ++t) th.emplace_back(work);
-    for (auto& t : th) t.join();
+    run_workers(nthreads, work);
     return 0;
 }
 

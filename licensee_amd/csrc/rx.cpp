@@ -290,9 +290,36 @@ struct Cont {
     virtual bool operator()(size_t pos) const = 0;
 };
 
+namespace {
+// Node frames per match: measured ~0.27 KiB of stack per frame (gcc -O3) (m -> seq/rep -> continuation),
+// so the default (main thread and other callers' threads, 8 MiB stacks) keeps well inside
+// 8 MiB; normalize.cpp raises it on its large-stack worker threads.
+constexpr size_t kDefaultMatchDepth = 12000;
+thread_local size_t tl_match_depth = kDefaultMatchDepth;
+}  // namespace
+
+size_t max_match_depth() { return tl_match_depth; }
+void set_match_depth(size_t frames) { tl_match_depth = frames ? frames : kDefaultMatchDepth; }
+
 struct Matcher {
     const Str& s;
     std::vector<long>& caps;
+    // Continuation-passing backtracking nests one set of frames per matched node: a repeated
+    // group such as the copyright pattern's (MAIN_LINE OPT*)+ goes deeper with every line it
+    // matches. Past max_match_depth() the match aborts with TooDeep (the caller sends the text
+    // to the Python path) instead of overflowing the thread's stack.
+    size_t depth = 0;
+    const size_t limit = max_match_depth();
+    struct Guard {
+        size_t& d;
+        explicit Guard(size_t& dd, size_t lim) : d(dd) {
+            if (++d > lim) {
+                --d;
+                throw TooDeep();
+            }
+        }
+        ~Guard() { --d; }
+    };
 
     bool lit(const Node* n, size_t pos) const {
         if (pos >= s.size()) return false;
@@ -315,6 +342,7 @@ struct Matcher {
 
     // match node n at pos, then continuation k
     bool m(const Node* n, size_t pos, const Cont& k) {
+        const Guard g(depth, limit);
         switch (n->kind) {
             case Node::LIT: return lit(n, pos) && k(pos + 1);
             case Node::ANY: return pos < s.size() && (n->dotall || s[pos] != '\n') && k(pos + 1);

@@ -21,6 +21,15 @@ using Str = std::u32string;
 
 enum Flags : int { IGNORECASE = 2, MULTILINE = 8, DOTALL = 16 };  // Python re flag values
 
+// Thrown by a match that would nest deeper than max_match_depth() node frames (see Matcher in
+// rx.cpp); callers treat the text as one for the Python path.
+struct TooDeep {};
+// Node-frame limit of one match on this thread: sized for the worker threads' stacks
+// (normalize.cpp runs batch preparation on threads with kWorkerStack bytes of stack) and
+// smaller on other threads (default 8 MiB stacks). set_match_depth() changes it per thread.
+size_t max_match_depth();
+void set_match_depth(size_t frames);
+
 struct Node;
 using NodeP = std::shared_ptr<Node>;
 

@@ -135,9 +135,12 @@ class License(ContentHelper):
 
     @classmethod
     def set_corpus(cls, licenses: List['License']):
-        """Install an explicit corpus (vendoring tool / tests); resets the title regex."""
+        """Install an explicit corpus (vendoring tool / tests); resets the title regex and the
+        process-wide Dice engine, whose resident templates belong to the previous corpus."""
         cls._corpus = list(licenses)
         cls._title_regex = None
+        from . import dice
+        dice.reset_default_engine()
 
     @classmethod
     def all(cls, hidden: bool = False, featured: Optional[bool] = None, pseudo: bool = True,

@@ -57,8 +57,9 @@ class Dice(Matcher):
     def potential_matches(self) -> List[License]:
         if not hasattr(self, '_potential'):
             fp = self.file.potential_false_positive()
+            # dice.rb:28 `license.wordset` excludes only nil: an empty Set is truthy in Ruby
             self._potential = [l for l in super().potential_matches()
-                               if not (l.creative_commons() and fp) and l.wordset()]
+                               if not (l.creative_commons() and fp) and l.wordset() is not None]
         return self._potential
 
     potential_licenses = potential_matches

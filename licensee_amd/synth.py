@@ -9,6 +9,7 @@ ids after -- and the C++ side composes files from token ids.
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from typing import List, Optional, Sequence
 
@@ -20,19 +21,12 @@ from .corpus import TemplateCorpus
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib', 'liblicensee_synth.so')
 
-# Lorem-ipsum filler words (the reference's add_random_words draws from a lorem-ipsum list,
-# spec_helper.rb:82-91); this list is our own.
-IPSUM_WORDS = (
-    'lorem ipsum dolor sit amet consectetur adipiscing elit sed do eiusmod tempor incididunt ut labore '
-    'et dolore magna aliqua enim ad minim veniam quis nostrud exercitation ullamco laboris nisi aliquip '
-    'ex ea commodo consequat duis aute irure in reprehenderit voluptate velit esse cillum fugiat nulla '
-    'pariatur excepteur sint occaecat cupidatat non proident sunt culpa qui officia deserunt mollit anim '
-    'id est laborum curabitur pretium tincidunt lacus nulla gravida orci a odio nullam varius turpis '
-    'morbi blandit cursus risus at ultrices mi tempus imperdiet vitae pellentesque habitant senectus '
-    'netus malesuada fames ac egestas integer feugiat scelerisque porta mauris sagittis vestibulum '
-    'faucibus interdum posuere praesent semper vulputate sapien nec aliquam viverra maecenas accumsan '
-    'lectus quam pulvinar etiam dignissim diam quis enim lobortis fermentum leo vel facilisis volutpat'
-).split()
+# Filler words: the reference's own list, spec/fixtures/ipsum.txt (924 words, repeats kept so
+# the draw weights match add_random_words, spec_helper.rb:82-91), vendored lowercased as
+# data/ipsum.json by tools/vendor_templates.py.
+IPSUM_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data', 'ipsum.json')
+with open(IPSUM_PATH, encoding='utf-8') as _fh:
+    IPSUM_WORDS = tuple(json.load(_fh)['words'])
 
 
 class _Spec(ctypes.Structure):

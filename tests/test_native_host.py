@@ -163,3 +163,31 @@ def test_batch_prep_matches_python(hp):
         assert cr[i] == (Copyright(lf).match() is not None), i
         e = Exact(lf).match()
         assert ex[i] == (keys.index(e.key) if e is not None else -1), i
+
+
+def test_thousands_of_copyright_lines(hp):
+    """A file opening with ~10k consecutive copyright lines (the copyright pattern's repeated
+    group, content_helper.rb:255 + copyright.rb:8-11, nests the backtracking matcher once per
+    line): batch workers (256 MiB stacks) finish it natively; on an ordinary 8 MiB thread the
+    match aborts at the frame limit and the text goes to the Python path. No crash, and every
+    result equals the Python LicenseFile path."""
+    from licensee_amd.matchers import Copyright, Exact
+    mit = License.find('mit').content_normalized()
+    texts = [''.join(f'Copyright (c) {1990 + i % 30} Holder Number {i} <h{i}@example.com>\n' for i in range(n)) + mit
+             for n in (50, 2_000, 10_000)]
+    texts.append('\n'.join(f'Copyright {i} Foo' for i in range(12_000)))   # copyright-only file
+    fb, cr, ex, fell = hp.prep_files(texts, ['LICENSE'] * len(texts), nthreads=4)
+    assert not fell.any()
+    corpus = hp.corpus
+    keys = [t.key for t in corpus.templates]
+    for i, t in enumerate(texts):
+        lf = LicenseFile(t, 'LICENSE')
+        bits, wf = corpus.intern(lf.wordset())
+        assert np.array_equal(fb.bits[i], bits) and fb.wordset_size[i] == wf and fb.length[i] == lf.length(), i
+        assert cr[i] == (Copyright(lf).match() is not None), i
+        e = Exact(lf).match()
+        assert ex[i] == (keys.index(e.key) if e is not None else -1), i
+    assert cr[3] and not cr[0]
+    # single-text entry point on this (8 MiB) thread: small texts native, the deep one falls back
+    assert hp.normalize(texts[0]) == LicenseFile(texts[0], 'LICENSE').content_normalized()
+    assert hp.normalize(texts[2]) is None

@@ -44,7 +44,9 @@ def generated_source(corpus) -> str:
     return buf.value.decode()
 
 
-def run_host(corpus, fb, k, tmp_path):
+def run_host(corpus, fb, k, tmp_path, with_votes=False):
+    """Run the generated kernels on the host; with ``with_votes`` also return the number of
+    64-file waves of the match kernel whose wave-wide vote chose the IEEE slow path."""
     src = generated_source(corpus)
     d = str(tmp_path)
     with open(os.path.join(d, 'prog.inc'), 'w') as fh:
@@ -62,13 +64,15 @@ def run_host(corpus, fb, k, tmp_path):
         pad = np.zeros(npad, dt)
         pad[:n] = arr
         pad.tofile(os.path.join(d, name + '.bin'))
-    subprocess.run([exe, d, str(n), str(k)], check=True)
+    out = subprocess.run([exe, d, str(n), str(k)], check=True, capture_output=True, text=True).stdout
+    slow_waves = int(out.split('slow_waves ')[1].split()[0])
     T = corpus.lf_bits.shape[0]
     rd = lambda name, dt: np.fromfile(os.path.join(d, name), dt)
-    return (rd('best.out', np.int32), rd('ov.out', np.uint32), rd('score.out', np.float64),
+    res = (rd('best.out', np.int32), rd('ov.out', np.uint32), rd('score.out', np.float64),
             # device matrix layout is template-major: [T][n] and [k][n]
             rd('mov.out', np.uint32).reshape(T, n).T, rd('msc.out', np.float64).reshape(T, n).T,
-            rd('tki.out', np.int32).reshape(max(k, 1), n)[:k].T, rd('tks.out', np.float64).reshape(max(k, 1), n)[:k].T)
+           rd('tki.out', np.int32).reshape(max(k, 1), n)[:k].T, rd('tks.out', np.float64).reshape(max(k, 1), n)[:k].T)
+    return res + (slow_waves,) if with_votes else res
 
 
 SCHEDULES = {
@@ -140,3 +144,67 @@ def test_exact_ties_later_key_wins(tmp_path, monkeypatch):
     matched = best[best >= 0]
     assert len(matched) > 50 and all(keys[b].startswith('zz-') for b in matched)
     assert all(keys[i].startswith('zz-') for i in tki[:, 0] if i >= 0)
+
+
+def _check_vs_oracle(corpus, fb, got, k):
+    from oracle.native import OracleScorer
+    best, ov, score, mov, msc, tki, tks = got
+    orc = OracleScorer(*corpus.arrays() if hasattr(corpus, 'arrays') else
+                       (corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                        corpus.length, corpus.is_cc), n_vocab=corpus.n_vocab)
+    # hash mode: the Set#& restatement, independent of the kernels' AND+popcount formulation
+    eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, mode=0)
+    assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+    emov, emsc = orc.matrix(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive)
+    assert np.array_equal(mov, emov) and np.array_equal(msc, emsc)
+    # top-k: the k best of the (CC-filtered) row in stable-ascending-then-reversed order
+    T = mov.shape[1]
+    for i in range(fb.n):
+        cand = [t for t in range(T) if not (corpus.is_cc[t] and fb.cc_false_positive[i])]
+        ranked = sorted(cand, key=lambda t: (emsc[i, t], t), reverse=True)[:k]
+        assert tki[i].tolist() == ranked + [-1] * (k - len(ranked)), i
+        assert tks[i, :len(ranked)].tolist() == [emsc[i, t] for t in ranked], i
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+def test_mixed_fast_slow_waves(tmp_path, monkeypatch):
+    """Waves that mix fast lanes with lanes outside the fast envelope (|W_F| >= 2^20 or
+    len_F >= 2^21) run MATCH_BODY(false) / MATRIX_BODY(false) -- the IEEE-double compares --
+    for all 64 lanes (the shim's __all is wave-wide); other waves keep the exact rational path.
+    Both must equal the oracle's hash mode bit for bit (content_helper.rb:128-133)."""
+    for key in ('DICE_PROG_SCHED', 'DICE_PROG_BURST', 'DICE_PROG_NT', 'DICE_PROG_QORDER'):
+        monkeypatch.delenv(key, raising=False)
+    from licensee_amd._native import FileBatch
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from tests.helpers import widen_lanes
+    templates = License.all(hidden=True, pseudo=False)
+    corpus = TemplateCorpus(templates)
+    fb0 = corpus.intern_files(make_files(templates, 1024, 8))
+    fb, idx = widen_lanes(fb0, seed=3)
+    # waves 8..15 stay entirely fast: the same run covers both vote outcomes
+    wf, ln = fb.wordset_size.copy(), fb.length.copy()
+    wf[512:], ln[512:] = fb0.wordset_size[512:], fb0.length[512:]
+    fb = FileBatch(fb.bits, wf, ln, fb.cc_false_positive)
+    got = run_host(corpus, fb, 5, tmp_path, with_votes=True)
+    assert got[-1] == 8, got[-1]
+    _check_vs_oracle(corpus, fb, got[:-1], 5)
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+def test_corpus_outside_fast_envelope(tmp_path, monkeypatch):
+    """A corpus breaking 200*|Lf| < 1024*base (and one template length >= 2^20) compiles with
+    CORPUS_FAST 0: every wave takes the IEEE-double path; scores above 100 occur."""
+    for key in ('DICE_PROG_SCHED', 'DICE_PROG_BURST', 'DICE_PROG_NT', 'DICE_PROG_QORDER'):
+        monkeypatch.delenv(key, raising=False)
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from tests.helpers import outside_fast_envelope
+    templates = License.all(hidden=True, pseudo=False)
+    corpus = outside_fast_envelope(TemplateCorpus(templates))
+    assert '#define CORPUS_FAST 0' in generated_source(corpus)
+    fb = TemplateCorpus(templates).intern_files(make_files(templates, 300, 12) + [NormFile('')])
+    got = run_host(corpus, fb, 4, tmp_path, with_votes=True)
+    assert got[-1] == (fb.n + 63) // 64
+    _check_vs_oracle(corpus, fb, got[:-1], 4)
+    assert (got[2] > 100.0).any()
