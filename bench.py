@@ -17,13 +17,15 @@ The JSON line also carries:
                   stream; peak 8000 GB/s (MI355X HBM3E). traffic = per-launch HBM bytes from
                   the committed rocprofv3 PMC pass (profiles/pmc_<config>.json) when present.
   cpu_baseline -- oracle/dice_ref.c (C port of the reference Set#& algorithm), rank 0 at N=1,
-                  on a bounded sample of the same files, threads stated.
-  parity       -- GPU results of the timed run vs the C oracle on that sample (bit-exact).
+                  on a bounded sample of the same files, on every core the process may use.
+  parity       -- GPU results of the timed run vs the C oracle's hash mode on that sample.
+  extras.configs -- at N=1, the other BASELINE configs (3: ~600 templates, LDS kernel; 4:
+                  long/mixed files; 5: full matrix + top-k) measured in the same run, each with
+                  its own HIP-event launch time, roofline fraction and oracle parity sample.
 """
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -36,10 +38,42 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'license files scored/sec (whole node) vs all templates; % HBM roofline'
 HBM_PEAK_GBS = 8000.0
+DEFAULT_FILES = {2: 1_000_000, 3: 1_250_000, 4: 1_000_000, 5: 1_000_000}
+KERNELS = ['dense', 'sparse-program', 'lds-sparse']
+WORKLOADS = {2: 'config2: synthetic perturbed LICENSE files x 47 choosealicense.com templates, Dice#match thr 98',
+             3: 'config3: synthetic files x ~600 synthetic templates (LDS-tiled sparse kernel), one GPU shard '
+                'of the 10M-file node run',
+             4: 'config4: long/mixed COPYING files (2-6 templates + notices) x 47 templates',
+             5: 'config5: full N x T similarity matrix + top-k x 47 templates'}
 
 
 def log(*a):
     print('[bench]', *a, file=sys.stderr, flush=True)
+
+
+def cpu_info():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            q, p = fh.read().split()[:2]
+            if q != 'max':
+                quota = max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {'threads': max(1, min(usable, 256)), 'affinity_cpus': affinity, 'cgroup_cpu_quota': quota,
+            'nproc': os.cpu_count(), 'cpu_model': model}
 
 
 def build_workload(config: int):
@@ -49,8 +83,118 @@ def build_workload(config: int):
     if config == 3:
         from licensee_amd.synth_templates import synthetic_templates
         templates = synthetic_templates(templates, 600, seed=20250202)
-    corpus = TemplateCorpus(templates)
-    return templates, corpus
+    return TemplateCorpus(templates)
+
+
+def traffic_for(cfg, n_per, T):
+    pmc_path = os.path.join(ROOT, 'profiles', f'pmc_config{cfg}.json')
+    if not os.path.exists(pmc_path):
+        return None, None
+    try:
+        with open(pmc_path) as fh:
+            pmc = json.load(fh)
+        if pmc.get('files_per_launch') == n_per and pmc.get('templates') == T:
+            return pmc.get('hbm_bytes_per_launch'), f"profiles/pmc_config{cfg}.json ({pmc.get('tag')})"
+    except Exception:
+        pass
+    return None, None
+
+
+class Run:
+    """One config's workload resident on the GPU: corpus, files, scorer, batch."""
+
+    def __init__(self, cfg, n_per, rank, world, dev, nthreads, args):
+        from licensee_amd._native import Scorer
+        from licensee_amd.shard import shard_range
+        from licensee_amd.synth import SyntheticCorpus
+        self.cfg, self.n_per, self.args = cfg, n_per, args
+        t0 = time.time()
+        self.corpus = build_workload(cfg)
+        self.synth = SyntheticCorpus(self.corpus, profile=1 if cfg == 4 else 0)
+        first, count = shard_range(rank, world, n_per)
+        self.files = self.synth.generate(first, count, seed=20250202, nthreads=nthreads)
+        log(f'config {cfg} rank {rank}: generated {n_per} files in {time.time() - t0:.1f}s '
+            f'(V={self.corpus.n_vocab}, T={len(self.corpus.templates)})')
+        c = self.corpus
+        self.scorer = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc,
+                             n_vocab=c.n_vocab, device=dev)
+        self.T, self.V, self.kind, self.entries = self.scorer.info()
+        self.batch = self.scorer.batch(n_per)
+        out_bytes = self.T * 12 + args.topk * 12 if cfg == 5 else 16
+        self.algo_bytes_per_file = self.batch.bytes_per_file() + 4 + 4 + 1 + out_bytes
+
+    def step(self, sptr):
+        if self.args.probe:
+            self.batch.stream_probe(sptr)
+        elif self.cfg == 5:
+            self.batch.matrix(self.args.topk, sptr)
+        else:
+            self.batch.match(self.args.threshold, sptr)
+
+    def close(self):
+        self.batch.close()
+        self.scorer.close()
+
+
+def timed(run, steps, warmup, stream, distributed):
+    """W untimed steps, then K steps between barrier + synchronize; HIP events on the launch
+    stream give the per-launch time; wall time and event time are max-reduced over ranks."""
+    import torch
+    import torch.distributed as dist
+    sptr = stream.cuda_stream
+    run.batch.upload(run.files, sptr)
+    torch.cuda.synchronize()
+    for _ in range(warmup):
+        run.step(sptr)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        run.step(sptr)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t_start
+    ev_ms = ev0.elapsed_time(ev1)
+    if distributed:
+        t = torch.tensor([wall, ev_ms], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, ev_ms = float(t[0]), float(t[1])
+    launch_ms = ev_ms / steps
+    achieved = run.algo_bytes_per_file * run.n_per / (launch_ms * 1e-3) / 1e9
+    return wall, launch_ms, achieved
+
+
+def oracle_for(corpus):
+    from oracle.native import OracleScorer
+    return OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                        corpus.length, corpus.is_cc, corpus.n_vocab)
+
+
+def parity_sample(run, orc, sptr, threads, n_sample):
+    """GPU results of the timed batch vs the C oracle's hash mode (Set#& restatement) on the
+    first n_sample files: match results, or for config 5 the matrix and its top-1."""
+    f = run.files
+    sl = slice(0, min(n_sample, run.n_per))
+    if run.cfg != 5:
+        best, ov, score = run.batch.download_match(sptr)
+        eb, eo, es = orc.match(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl],
+                               run.args.threshold, nthreads=threads, mode=0)
+        mism = int(np.sum(best[sl] != eb) + np.sum(ov[sl] != eo) + np.sum(score[sl] != es))
+        return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
+    ovm, scm, tki, tks = run.batch.download_matrix(run.args.topk, sptr)
+    mov, msc = orc.matrix(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl], nthreads=threads)
+    mism = int(np.sum(ovm[sl] != mov) + np.sum(scm[sl] != msc))
+    rows = np.arange(sl.stop)
+    mism += int(np.sum(scm[rows, tki[sl, 0]] != tks[sl, 0]))
+    return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (matrix, hash Set#&)'}
 
 
 def main():
@@ -64,6 +208,8 @@ def main():
     ap.add_argument('--topk', type=int, default=3)
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU-work budget of the baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--extra-configs', default='3,4,5',
+                    help="configs also measured at N=1 (reported under extras.configs); '' for none")
     ap.add_argument('--probe', action='store_true', help='diagnostic: stream-read the tiles only (read ceiling)')
     args = ap.parse_args()
 
@@ -87,88 +233,22 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
-
-    from licensee_amd.synth import SyntheticCorpus
-    from licensee_amd._native import Scorer
+    cpu = cpu_info()
+    nthreads = min(16, cpu['threads'])            # generator / host-prep threads (box CPU share)
 
     cfg = args.config
-    default_files = {2: 1_000_000, 3: 1_250_000, 4: 1_000_000, 5: 1_000_000}[cfg]
-    n_per = args.files_per_gpu or default_files
-    templates, corpus = build_workload(cfg)
-    synth = SyntheticCorpus(corpus, profile=1 if cfg == 4 else 0)
-    nthreads = min(16, os.cpu_count() or 1)
-    t0 = time.time()
-    from licensee_amd.shard import shard_range
-    first, count = shard_range(rank, world, n_per)
-    files = synth.generate(first, count, seed=20250202, nthreads=nthreads)
-    log(f'rank {rank}: generated {n_per} files in {time.time() - t0:.1f}s (V={corpus.n_vocab}, T={len(templates)})')
-
-    scorer = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
-                    corpus.is_cc, n_vocab=corpus.n_vocab, device=dev)
-    T, V, kind, entries = scorer.info()
-    batch = scorer.batch(n_per)
+    n_per = args.files_per_gpu or DEFAULT_FILES[cfg]
+    run = Run(cfg, n_per, rank, world, dev, nthreads, args)
     stream = torch.cuda.Stream()          # a real (non-null) stream: kernels and HIP events share it
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    batch.upload(files, sptr)
-    torch.cuda.synchronize()
-
-    def step():
-        if args.probe:
-            batch.stream_probe(sptr)
-        elif cfg == 5:
-            batch.matrix(args.topk, sptr)
-        else:
-            batch.match(args.threshold, sptr)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t_start = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t_start
-    ev_ms = ev0.elapsed_time(ev1)
-    if distributed:
-        t = torch.tensor([wall, ev_ms], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, ev_ms = float(t[0]), float(t[1])
-
+    wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, distributed)
     total_files = n_per * world
     value = total_files * args.steps / wall
-    launch_ms = ev_ms / args.steps
-    tile_bytes = batch.bytes_per_file()
-    if cfg == 5:
-        out_bytes = T * 12 + args.topk * 12
-    else:
-        out_bytes = 16
-    algo_bytes_per_file = tile_bytes + 4 + 4 + 1 + out_bytes
-    achieved = algo_bytes_per_file * n_per / (launch_ms * 1e-3) / 1e9
-    traffic = None
-    traffic_src = None
-    pmc_path = os.path.join(ROOT, 'profiles', f'pmc_config{cfg}.json')
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as fh:
-                pmc = json.load(fh)
-            if pmc.get('files_per_launch') == n_per and pmc.get('templates') == T:
-                traffic = pmc.get('hbm_bytes_per_launch')
-                traffic_src = f"profiles/pmc_config{cfg}.json ({pmc.get('tag')})"
-        except Exception:
-            traffic = None
+    traffic, traffic_src = traffic_for(cfg, n_per, run.T)
+    batch, files, corpus, synth = run.batch, run.files, run.corpus, run.synth
 
-    # ---- results: parity + gathers (outside the timed region) -------------------------
+    # ---- results: gathers (outside the timed region) -------------------------
     extras = {}
     if cfg != 5:
         t_g = time.perf_counter()
@@ -177,20 +257,10 @@ def main():
         extras['host_gather_ms'] = host_gather_s * 1e3
         extras['matches'] = int((best >= 0).sum())
         if distributed:
-            # RCCL alternative: all_gather the 16-B/file results over xGMI
-            res = torch.empty((n_per, 4), dtype=torch.int32, device='cuda')
-            hip = ctypes.CDLL('libamdhip64.so.7')   # by soname: the runtime torch already loaded
-            pb, po, ps = batch.result_ptrs()
-            hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-            tmp_b = torch.empty(n_per, dtype=torch.int32, device='cuda')
-            tmp_o = torch.empty(n_per, dtype=torch.int32, device='cuda')
-            tmp_s = torch.empty(n_per, dtype=torch.float64, device='cuda')
-            hip.hipMemcpy(tmp_b.data_ptr(), pb, n_per * 4, 3)
-            hip.hipMemcpy(tmp_o.data_ptr(), po, n_per * 4, 3)
-            hip.hipMemcpy(tmp_s.data_ptr(), ps, n_per * 8, 3)
-            res[:, 0] = tmp_b
-            res[:, 1] = tmp_o
-            res[:, 2:4] = tmp_s.view(torch.int32).view(n_per, 2)
+            # RCCL alternative: all_gather the 16-B/file results over xGMI (zero-copy views of the
+            # library's result buffers, packed on the device: licensee_amd/shard.py)
+            from licensee_amd.shard import device_results_packed
+            res = device_results_packed(batch)
             out = torch.empty((world * n_per, 4), dtype=torch.int32, device='cuda')
             torch.cuda.synchronize()
             dist.barrier()
@@ -222,7 +292,7 @@ def main():
         extras['host_prep_python_files_per_s'] = len(sample) / (time.perf_counter() - t_h)
         from licensee_amd.native_host import HostPrep
         hp = HostPrep(corpus)
-        big = [synth.text(i)[0] for i in range(2000)]
+        big = [synth.text(i)[0] for i in range(4000)]
         t_h = time.perf_counter()
         hp.prep_files(big, None, nthreads=nthreads)
         extras['host_prep_native_files_per_s'] = len(big) / (time.perf_counter() - t_h)
@@ -232,10 +302,9 @@ def main():
     cpu_baseline = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle.native import OracleScorer, bits_to_csr
-        orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
-                           corpus.length, corpus.is_cc, corpus.n_vocab)
-        cpu_threads = nthreads
+        from oracle.native import bits_to_csr
+        orc = oracle_for(corpus)
+        cpu_threads = cpu['threads']
         # calibrate on a small slice, then size the sample to ~cpu_seconds of CPU work
         cal = min(n_per, 4000)
         csr = bits_to_csr(files.bits[:cal], corpus.n_vocab)
@@ -257,43 +326,67 @@ def main():
         cpu_baseline = {'value': sample / cpu_s, 'unit': 'files/s', 'cores': cpu_threads, 'kind': 'port',
                         'sample': f'first {sample} files of the same synthetic workload, hash-set Set#& '
                                   f'restatement (oracle/dice_ref.c), {cpu_threads} threads',
-                        'bitset_variant_files_per_s': sample / cpu_bits_s}
+                        'bitset_variant_files_per_s': sample / cpu_bits_s,
+                        'nproc': cpu['nproc'], 'affinity_cpus': cpu['affinity_cpus'],
+                        'cgroup_cpu_quota': cpu['cgroup_cpu_quota'], 'cpu_model': cpu['cpu_model']}
         if cfg != 5:
             mism = int(np.sum(best[sl] != cb) + np.sum(ov[sl] != co) + np.sum(score[sl] != cs))
-            parity = {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c'}
+            parity = {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
         else:
-            ovm, scm, tki, tks = batch.download_matrix(args.topk, sptr)
-            mov, msc = orc.matrix(files.bits[sl], files.wordset_size[sl], files.length[sl],
-                                  files.cc_false_positive[sl], nthreads=cpu_threads)
-            mism = int(np.sum(ovm[sl] != mov) + np.sum(scm[sl] != msc))
-            parity = {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (matrix)'}
+            parity = parity_sample(run, orc, sptr, cpu_threads, sample)
+
+    head = {'templates': run.T, 'vocab': run.V, 'kernel': KERNELS[run.kind], 'program_entries': run.entries,
+            'algorithmic_bytes_per_file': run.algo_bytes_per_file}
+    # ---- the other BASELINE configs, same run (N = 1) ---------------------------------------
+    if rank == 0 and world == 1 and not args.probe and args.extra_configs:
+        run.close()
+        run = None
+        extras['configs'] = {}
+        for c in [int(x) for x in args.extra_configs.split(',') if x.strip()]:
+            if c == cfg:
+                continue
+            r = Run(c, DEFAULT_FILES[c], 0, 1, dev, nthreads, args)
+            steps = min(args.steps, 20)
+            w, lm, ach = timed(r, steps, 2, stream, False)
+            tr, tr_src = traffic_for(c, r.n_per, r.T)
+            rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'templates': r.T, 'vocab': r.V,
+                   'kernel': KERNELS[r.kind], 'steps': steps, 'files_per_s': r.n_per * steps / w,
+                   'scores_per_s': r.n_per * steps / w * r.T, 'launch_ms': lm,
+                   'algorithmic_bytes_per_file': r.algo_bytes_per_file, 'roofline_achieved_gbs': ach,
+                   'roofline_frac': ach / HBM_PEAK_GBS, 'traffic': tr, 'traffic_source': tr_src}
+            if not args.no_cpu_baseline:
+                rec['parity'] = parity_sample(r, oracle_for(r.corpus), sptr, cpu['threads'],
+                                              {3: 20_000, 4: 30_000, 5: 50_000}[c])
+            extras['configs'][str(c)] = rec
+            log(f"config {c}: {rec['files_per_s']:.3e} files/s, launch {lm * 1e3:.1f} us, "
+                f"frac {rec['roofline_frac']:.3f}, parity {rec.get('parity')}")
+            r.close()
 
     if rank == 0:
-        workload = {2: 'config2: synthetic perturbed LICENSE files x 47 choosealicense.com templates, Dice#match thr 98',
-                    3: 'config3: synthetic files x ~600 synthetic templates (LDS-tiled sparse kernel)',
-                    4: 'config4: long/mixed COPYING files (2-6 templates + notices) x 47 templates',
-                    5: f'config5: full N x T similarity matrix + top-{args.topk} x 47 templates'}[cfg]
         line = {
             'metric': METRIC, 'value': value, 'unit': 'files/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': wall / args.steps * 1e3, 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
-            'data': 'synthetic (normalized-space perturbations of the vendored templates, seed 20250202)',
-            'config': {'workload': workload, 'files_per_gpu': n_per, 'global_files': total_files,
-                       'templates': T, 'vocab': V, 'kernel': ['dense', 'sparse-program', 'lds-sparse'][kind],
-                       'program_entries': entries, 'parallelism': f'shard{world}'},
+            'data': 'synthetic (normalized-space perturbations of the vendored templates, filler words from '
+                    'the reference spec/fixtures/ipsum.txt, seed 20250202)',
+            'config': {'workload': WORKLOADS[cfg], 'files_per_gpu': n_per, 'global_files': total_files,
+                       'templates': head['templates'], 'vocab': head['vocab'], 'kernel': head['kernel'],
+                       'program_entries': head['program_entries'], 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'traffic_source': traffic_src,
-                         'algorithmic_bytes_per_file': algo_bytes_per_file, 'launch_ms': launch_ms,
+                         'algorithmic_bytes_per_file': head['algorithmic_bytes_per_file'], 'launch_ms': launch_ms,
                          **({'note': 'config 3 is compute-bound (VALU/LDS issue of the LDS-tiled kernel); '
-                                     'frac is its HBM share only (DESIGN.md 4b)'} if kind == 2 else {})},
+                                     'frac is its HBM share only (DESIGN.md 4b)'} if cfg == 3 else {})},
             'cpu_baseline': cpu_baseline,
-            'scores_per_s': value * T,
+            'scores_per_s': value * head['templates'],
             'parity': parity,
             'extras': extras,
         }
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + '\n').encode())
+    if run is not None:
+        run.close()
     if distributed:
         dist.destroy_process_group()
 

@@ -17,6 +17,8 @@
  *   dice_similarity_matrix          Dice#matches_by_similarity / #licenses_by_similarity (full N x T
  *                                   scores + sorted top-k, no threshold cut)  dice.rb:34-41;
  *                                   also `licensee detect` "closest licenses" lib/licensee/commands/detect.rb:96-106
+ *   dice_*_sharded                  the same two calls with the files sharded over several
+ *                                   devices of one node (the dice.rb:34-41 loop is per file)
  *   dice_batch_*                    device-resident batch variants of the two calls above
  *   dice_last_error                 replaces the Ruby exceptions of the path (license.rb:258,
  *                                   content_helper.rb:230,310) with status codes + message
@@ -107,6 +109,26 @@ int dice_match(dice_ctx *ctx, const dice_files *files, double threshold,
 int dice_similarity_matrix(dice_ctx *ctx, const dice_files *files,
                            uint32_t *overlap, double *score,
                            int32_t k, int32_t *topk_index, double *topk_score);
+
+/* ---- one node, several devices: the files of one call sharded over contexts ----------
+ * The loop of Dice#matches_by_similarity (dice.rb:34-41) is independent per file, so a call
+ * splits its files into n_ctx contiguous shards (shard i = files [n*i/n_ctx, n*(i+1)/n_ctx)),
+ * each scored by ctxs[i] on its own device, host thread and stream; templates are replicated
+ * (every ctx must hold the same corpus: same T and V, checked; same bitsets, not checked).
+ * Only results move:
+ *   DICE_GATHER_HOST    every device copies its results straight into its disjoint slice of
+ *                       the caller's buffers (parallel D2H);
+ *   DICE_GATHER_DEVICE  every device copies its results into one buffer on ctxs[0]'s device
+ *                       (peer copies over xGMI), then one D2H from there.
+ * Several ctxs may share a device (tests on a one-GPU box). Results are bit-identical to the
+ * single-ctx calls. Outputs as dice_match / dice_similarity_matrix. */
+#define DICE_GATHER_HOST 0
+#define DICE_GATHER_DEVICE 1
+int dice_match_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files, double threshold,
+                       int32_t gather_mode, int32_t *best, uint32_t *overlap, double *score);
+int dice_similarity_matrix_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files,
+                                   int32_t gather_mode, uint32_t *overlap, double *score, int32_t k,
+                                   int32_t *topk_index, double *topk_score);
 
 /* ---- device-resident batches (inputs and results stay in HBM) ---------------------- */
 int dice_batch_create(dice_ctx *ctx, int64_t capacity, dice_batch **out);

@@ -24,7 +24,10 @@ EXPORTED_SYMBOLS = (
     'dice_batch_match', 'dice_batch_matrix', 'dice_batch_download_match',
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
     'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
+    'dice_match_sharded', 'dice_similarity_matrix_sharded',
 )
+DICE_GATHER_HOST = 0
+DICE_GATHER_DEVICE = 1
 
 
 class DiceError(RuntimeError):
@@ -74,6 +77,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_bytes_per_file': (i64, [vp]),
         'dice_batch_stream_probe': (ctypes.c_int, [vp, vp]),
         'dice_last_error': (ctypes.c_char_p, []),
+        'dice_match_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), ctypes.c_double, i32, vp, vp, vp]),
+        'dice_similarity_matrix_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), i32, vp, vp, i32,
+                                                          vp, vp]),
         'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
         'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
     }
@@ -254,3 +260,43 @@ class DeviceBatch:
 
     def bytes_per_file(self) -> int:
         return int(load_library().dice_batch_bytes_per_file(self._b))
+
+
+def _ctx_array(scorers):
+    scorers = list(scorers)
+    if not scorers:
+        raise ValueError('need at least one Scorer')
+    arr = (ctypes.c_void_p * len(scorers))(*[sc._ctx.value for sc in scorers])
+    return arr, len(scorers), scorers[0].n_templates
+
+
+def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DICE_GATHER_HOST):
+    """``dice_match_sharded``: the files split into contiguous shards, one per Scorer (each on
+    its own device, host thread and stream), results gathered on the host or on the first
+    Scorer's device. Every Scorer must hold the same corpus."""
+    arr, n_ctx, _ = _ctx_array(scorers)
+    n = files.n
+    best = np.empty(n, np.int32)
+    ov = np.empty(n, np.uint32)
+    score = np.empty(n, np.float64)
+    if n:
+        st = files._struct()
+        _check(load_library().dice_match_sharded(arr, n_ctx, ctypes.byref(st), float(threshold), int(gather),
+                                                 _ptr(best), _ptr(ov), _ptr(score)))
+    return best, ov, score
+
+
+def matrix_sharded(scorers, files: FileBatch, k: int = 0, gather: int = DICE_GATHER_HOST):
+    """``dice_similarity_matrix_sharded``: full [n][T] matrix + [n][k] top-k, sharded."""
+    arr, n_ctx, T = _ctx_array(scorers)
+    n = files.n
+    ov = np.empty((n, T), np.uint32)
+    score = np.empty((n, T), np.float64)
+    tki = np.empty((n, max(k, 0)), np.int32)
+    tks = np.empty((n, max(k, 0)), np.float64)
+    if n:
+        st = files._struct()
+        _check(load_library().dice_similarity_matrix_sharded(arr, n_ctx, ctypes.byref(st), int(gather), _ptr(ov),
+                                                             _ptr(score), int(k), _ptr(tki) if k else None,
+                                                             _ptr(tks) if k else None))
+    return ov, score, tki, tks

@@ -283,8 +283,10 @@ int dalloc(T** p, size_t count) {
 static hipStream_t pick_stream(dice_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
 
 template <class E>
-static int transpose_to_host(dice_batch* b, const E* d_src, int64_t rows, int64_t cols, E* host, hipStream_t s) {
-    // rows x cols (template-major) -> cols x rows on device, then D2H
+static int transpose_to(dice_batch* b, const E* d_src, int64_t rows, int64_t cols, E* dst, hipStream_t s,
+                        hipMemcpyKind kind) {
+    // rows x cols (template-major) -> cols x rows on device, then a copy to `dst` (host memory,
+    // or another device's memory for the sharded device gather)
     const size_t bytes = (size_t)rows * cols * sizeof(E);
     if (b->stage_bytes < bytes) {
         if (b->d_stage) (void)hipFree(b->d_stage);
@@ -296,7 +298,7 @@ static int transpose_to_host(dice_batch* b, const E* d_src, int64_t rows, int64_
     dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
     hipLaunchKernelGGL(dice_transpose<E>, grid, dim3(256), 0, s, d_src, (E*)b->d_stage, rows, cols);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(host, b->d_stage, bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(dst, b->d_stage, bytes, kind, s));
     HIP_TRY(hipStreamSynchronize(s));
     return DICE_OK;
 }
@@ -539,19 +541,45 @@ int dice_batch_matrix(dice_batch* b, int32_t k, void* stream) {
     return DICE_OK;
 }
 
+}  // extern "C"
+
+namespace dice {
+
+int download_match_to(dice_batch* b, int32_t* best, uint32_t* ov, double* score, hipStream_t s,
+                      hipMemcpyKind kind) {
+    const size_t n = (size_t)b->n;
+    if (n) {
+        if (best) HIP_TRY(hipMemcpyAsync(best, b->d_best, n * 4, kind, s));
+        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_ov, n * 4, kind, s));
+        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_score, n * 8, kind, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return DICE_OK;
+}
+
+int download_matrix_to(dice_batch* b, uint32_t* ov, double* score, int32_t* tki, double* tks, hipStream_t s,
+                       hipMemcpyKind kind) {
+    dice_ctx* c = b->ctx;
+    const int64_t n = b->n;
+    if (n && !b->d_mov) return fail(DICE_E_STATE, "dice_batch_matrix was not run");
+    if (!n) return DICE_OK;
+    int rc;
+    if (ov && (rc = transpose_to<uint32_t>(b, b->d_mov, c->T, n, ov, s, kind))) return rc;
+    if (score && (rc = transpose_to<double>(b, b->d_mscore, c->T, n, score, s, kind))) return rc;
+    if (tki && b->k_used && (rc = transpose_to<int32_t>(b, b->d_tki, b->k_used, n, tki, s, kind))) return rc;
+    if (tks && b->k_used && (rc = transpose_to<double>(b, b->d_tks, b->k_used, n, tks, s, kind))) return rc;
+    return DICE_OK;
+}
+
+}  // namespace dice
+
+extern "C" {
+
 int dice_batch_download_match(dice_batch* b, int32_t* best, uint32_t* ov, double* score, void* stream) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
     dice_ctx* c = b->ctx;
     DeviceGuard g(c->device);
-    hipStream_t s = pick_stream(c, stream);
-    const size_t n = (size_t)b->n;
-    if (n) {
-        if (best) HIP_TRY(hipMemcpyAsync(best, b->d_best, n * 4, hipMemcpyDeviceToHost, s));
-        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_ov, n * 4, hipMemcpyDeviceToHost, s));
-        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_score, n * 8, hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipStreamSynchronize(s));
-    return DICE_OK;
+    return dice::download_match_to(b, best, ov, score, pick_stream(c, stream), hipMemcpyDeviceToHost);
 }
 
 int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32_t k, int32_t* tki, double* tks,
@@ -562,16 +590,7 @@ int dice_batch_download_matrix(dice_batch* b, uint32_t* ov, double* score, int32
                                     std::to_string(b->k_used) + ")");
     dice_ctx* c = b->ctx;
     DeviceGuard g(c->device);
-    hipStream_t s = pick_stream(c, stream);
-    const int64_t n = b->n;
-    if (n && !b->d_mov) return fail(DICE_E_STATE, "dice_batch_matrix was not run");
-    if (!n) return DICE_OK;
-    int rc;
-    if (ov && (rc = transpose_to_host<uint32_t>(b, b->d_mov, c->T, n, ov, s))) return rc;
-    if (score && (rc = transpose_to_host<double>(b, b->d_mscore, c->T, n, score, s))) return rc;
-    if (tki && b->k_used && (rc = transpose_to_host<int32_t>(b, b->d_tki, b->k_used, n, tki, s))) return rc;
-    if (tks && b->k_used && (rc = transpose_to_host<double>(b, b->d_tks, b->k_used, n, tks, s))) return rc;
-    return DICE_OK;
+    return dice::download_matrix_to(b, ov, score, tki, tks, pick_stream(c, stream), hipMemcpyDeviceToHost);
 }
 
 int dice_batch_stream_probe(dice_batch* b, void* stream) {
@@ -598,7 +617,9 @@ int dice_batch_result_ptrs(dice_batch* b, void** best, void** ov, void** score) 
     return DICE_OK;
 }
 
-static int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out) {
+}  // extern "C"
+
+int dice::scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out) {
     if (ctx->scratch && ctx->scratch->capacity >= n) {
         *out = ctx->scratch;
         return DICE_OK;
@@ -612,11 +633,13 @@ static int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out) {
     return rc;
 }
 
+extern "C" {
+
 int dice_match(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
     if (!ctx || !f) return fail(DICE_E_ARG, "NULL ctx/files");
     if (f->n_files == 0) return DICE_OK;
     dice_batch* b = nullptr;
-    int rc = scratch_for(ctx, f->n_files, &b);
+    int rc = dice::scratch_for(ctx, f->n_files, &b);
     if (rc) return rc;
     if ((rc = dice_batch_upload(b, f, nullptr))) return rc;
     if ((rc = dice_batch_match(b, thr, nullptr))) return rc;
@@ -630,7 +653,7 @@ int dice_similarity_matrix(dice_ctx* ctx, const dice_files* f, uint32_t* ov, dou
     if (k > 0 && (!tki || !tks)) return fail(DICE_E_ARG, "top-k outputs required when k > 0");
     if (f->n_files == 0) return DICE_OK;
     dice_batch* b = nullptr;
-    int rc = scratch_for(ctx, f->n_files, &b);
+    int rc = dice::scratch_for(ctx, f->n_files, &b);
     if (rc) return rc;
     if ((rc = dice_batch_upload(b, f, nullptr))) return rc;
     if ((rc = dice_batch_matrix(b, k, nullptr))) return rc;

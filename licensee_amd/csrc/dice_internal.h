@@ -56,6 +56,14 @@ struct dice_ctx {
 namespace dice {
 int lds_setup(dice_ctx* c, const dice_templates* t);
 int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+// the ctx's reusable batch for the host-buffer calls (grown on demand)
+int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out);
+// result downloads to host memory or (kind hipMemcpyDefault) another device's memory;
+// synchronize `s`
+int download_match_to(dice_batch* b, int32_t* best, uint32_t* ov, double* score, hipStream_t s,
+                      hipMemcpyKind kind);
+int download_matrix_to(dice_batch* b, uint32_t* ov, double* score, int32_t* tki, double* tks, hipStream_t s,
+                       hipMemcpyKind kind);
 }  // namespace dice
 
 struct dice_batch {

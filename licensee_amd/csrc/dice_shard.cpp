@@ -1,0 +1,189 @@
+// One call, several devices: dice_match_sharded / dice_similarity_matrix_sharded
+// (include/licensee_dice.h). The per-file loop of Dice#matches_by_similarity
+// (lib/licensee/matchers/dice.rb:34-41) has no cross-file state, so the files of a call are
+// split into contiguous shards, one per ctx; each shard runs on its ctx's device from its own
+// host thread and stream (upload, kernel, download) and only results move.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/licensee_dice.h"
+#include "dice_internal.h"
+
+using dice::fail;
+
+namespace {
+
+struct Shard {
+    int64_t lo = 0, hi = 0;
+    int rc = DICE_OK;
+    std::string err;
+};
+
+int check_ctxs(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, int32_t gather) {
+    if (!ctxs || n_ctx < 1 || !f) return fail(DICE_E_ARG, "NULL ctxs/files or n_ctx < 1");
+    if (gather != DICE_GATHER_HOST && gather != DICE_GATHER_DEVICE) return fail(DICE_E_ARG, "unknown gather_mode");
+    for (int32_t i = 0; i < n_ctx; ++i) {
+        if (!ctxs[i]) return fail(DICE_E_ARG, "NULL ctx in ctxs");
+        if (ctxs[i]->T != ctxs[0]->T || ctxs[i]->V != ctxs[0]->V)
+            return fail(DICE_E_ARG, "ctxs hold different corpora (T or V differ)");
+    }
+    if (f->n_files < 0) return fail(DICE_E_ARG, "n_files < 0");
+    return DICE_OK;
+}
+
+dice_files slice(const dice_files* f, int64_t lo, int64_t hi, int32_t w64) {
+    dice_files s;
+    s.n_files = hi - lo;
+    s.bits = f->bits + (size_t)lo * w64;
+    s.wordset_size = f->wordset_size + lo;
+    s.length = f->length + lo;
+    s.cc_false_positive = f->cc_false_positive + lo;
+    return s;
+}
+
+// Runs fn(i, shard) for every ctx on its own thread (device set per thread) and returns the
+// first failing shard's status, its message moved to the calling thread's dice_last_error.
+template <class F>
+int run_shards(dice_ctx* const* ctxs, int32_t n_ctx, int64_t n, F&& fn) {
+    std::vector<Shard> sh((size_t)n_ctx);
+    for (int32_t i = 0; i < n_ctx; ++i) {
+        sh[i].lo = n * i / n_ctx;
+        sh[i].hi = n * (i + 1) / n_ctx;
+    }
+    auto body = [&](int32_t i) {
+        if (hipSetDevice(ctxs[i]->device) != hipSuccess) {
+            sh[i].rc = DICE_E_DEVICE;
+            sh[i].err = "hipSetDevice failed";
+            return;
+        }
+        sh[i].rc = sh[i].hi > sh[i].lo ? fn(i, sh[i]) : DICE_OK;
+        if (sh[i].rc != DICE_OK) sh[i].err = dice::last_error();
+    };
+    std::vector<std::thread> th;
+    for (int32_t i = 1; i < n_ctx; ++i) th.emplace_back(body, i);
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    body(0);
+    for (auto& t : th) t.join();
+    if (prev >= 0) (void)hipSetDevice(prev);
+    for (auto& s : sh)
+        if (s.rc != DICE_OK) return fail(s.rc, s.err);
+    return DICE_OK;
+}
+
+// Device gather buffer on ctxs[0]'s device: `bytes` bytes, freed by the caller.
+int gather_alloc(dice_ctx* c0, size_t bytes, void** p) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(c0->device) != hipSuccess) return fail(DICE_E_DEVICE, "hipSetDevice failed");
+    const hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail(DICE_E_NOMEM, "gather buffer allocation failed");
+    }
+    return DICE_OK;
+}
+
+// One D2H per output array from the device gather buffer (regions laid out back to back).
+int gather_d2h(dice_ctx* c0, const std::vector<std::pair<void*, size_t>>& outs, char* dev) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(c0->device) != hipSuccess) return fail(DICE_E_DEVICE, "hipSetDevice failed");
+    size_t off = 0;
+    hipError_t e = hipSuccess;
+    for (auto& o : outs) {
+        if (o.first && e == hipSuccess) e = hipMemcpyAsync(o.first, dev + off, o.second, hipMemcpyDeviceToHost, c0->stream);
+        off += o.second;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return e == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, std::string("gather D2H: ") + hipGetErrorString(e));
+}
+
+}  // namespace
+
+extern "C" {
+
+int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, double thr, int32_t gather,
+                       int32_t* best, uint32_t* ov, double* score) {
+    int rc = check_ctxs(ctxs, n_ctx, f, gather);
+    if (rc) return rc;
+    const int64_t n = f->n_files;
+    if (n == 0) return DICE_OK;
+    if (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive) return fail(DICE_E_ARG, "NULL file arrays");
+    const int32_t w64 = ctxs[0]->w64;
+    char* dev = nullptr;
+    if (gather == DICE_GATHER_DEVICE && (rc = gather_alloc(ctxs[0], (size_t)n * 16, (void**)&dev))) return rc;
+    // device gather layout: best [n] i32 | overlap [n] u32 | score [n] f64
+    int32_t* g_best = dev ? (int32_t*)dev : nullptr;
+    uint32_t* g_ov = dev ? (uint32_t*)(dev + (size_t)n * 4) : nullptr;
+    double* g_score = dev ? (double*)(dev + (size_t)n * 8) : nullptr;
+    rc = run_shards(ctxs, n_ctx, n, [&](int32_t i, Shard& s) {
+        dice_ctx* c = ctxs[i];
+        dice_batch* b = nullptr;
+        int r = dice::scratch_for(c, s.hi - s.lo, &b);
+        if (r) return r;
+        const dice_files part = slice(f, s.lo, s.hi, w64);
+        if ((r = dice_batch_upload(b, &part, nullptr)) || (r = dice_batch_match(b, thr, nullptr))) return r;
+        if (dev)
+            return dice::download_match_to(b, best ? g_best + s.lo : nullptr, ov ? g_ov + s.lo : nullptr,
+                                           score ? g_score + s.lo : nullptr, c->stream, hipMemcpyDefault);
+        return dice::download_match_to(b, best ? best + s.lo : nullptr, ov ? ov + s.lo : nullptr,
+                                       score ? score + s.lo : nullptr, c->stream, hipMemcpyDeviceToHost);
+    });
+    if (rc == DICE_OK && dev)
+        rc = gather_d2h(ctxs[0], {{best, (size_t)n * 4}, {ov, (size_t)n * 4}, {score, (size_t)n * 8}}, dev);
+    if (dev) (void)hipFree(dev);
+    return rc;
+}
+
+int dice_similarity_matrix_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, int32_t gather,
+                                   uint32_t* ov, double* score, int32_t k, int32_t* tki, double* tks) {
+    int rc = check_ctxs(ctxs, n_ctx, f, gather);
+    if (rc) return rc;
+    if (k < 0 || k > DICE_TOPK_MAX) return fail(DICE_E_ARG, "k out of range");
+    if (k > 0 && (!tki || !tks)) return fail(DICE_E_ARG, "top-k outputs required when k > 0");
+    const int64_t n = f->n_files;
+    if (n == 0) return DICE_OK;
+    if (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive) return fail(DICE_E_ARG, "NULL file arrays");
+    const int32_t w64 = ctxs[0]->w64, T = ctxs[0]->T;
+    if (k == 0) tki = nullptr, tks = nullptr;
+    // device gather layout (row-major, as the ABI): overlap [n][T] u32 | score [n][T] f64 |
+    // top-k index [n][k] i32 | top-k score [n][k] f64
+    const size_t b_ov = (size_t)n * T * 4, b_sc = (size_t)n * T * 8, b_ki = (size_t)n * k * 4, b_ks = (size_t)n * k * 8;
+    char* dev = nullptr;
+    if (gather == DICE_GATHER_DEVICE && (rc = gather_alloc(ctxs[0], b_ov + b_sc + b_ki + b_ks, (void**)&dev)))
+        return rc;
+    rc = run_shards(ctxs, n_ctx, n, [&](int32_t i, Shard& s) {
+        dice_ctx* c = ctxs[i];
+        dice_batch* b = nullptr;
+        int r = dice::scratch_for(c, s.hi - s.lo, &b);
+        if (r) return r;
+        const dice_files part = slice(f, s.lo, s.hi, w64);
+        if ((r = dice_batch_upload(b, &part, nullptr)) || (r = dice_batch_matrix(b, k, nullptr))) return r;
+        const size_t lo = (size_t)s.lo;
+        if (dev) {
+            uint32_t* d_ov = (uint32_t*)dev;
+            double* d_sc = (double*)(dev + b_ov);
+            int32_t* d_ki = (int32_t*)(dev + b_ov + b_sc);
+            double* d_ks = (double*)(dev + b_ov + b_sc + b_ki);
+            return dice::download_matrix_to(b, ov ? d_ov + lo * T : nullptr, score ? d_sc + lo * T : nullptr,
+                                            tki ? d_ki + lo * k : nullptr, tks ? d_ks + lo * k : nullptr, c->stream,
+                                            hipMemcpyDefault);
+        }
+        return dice::download_matrix_to(b, ov ? ov + lo * T : nullptr, score ? score + lo * T : nullptr,
+                                        tki ? tki + lo * k : nullptr, tks ? tks + lo * k : nullptr, c->stream,
+                                        hipMemcpyDeviceToHost);
+    });
+    if (rc == DICE_OK && dev)
+        rc = gather_d2h(ctxs[0], {{ov, b_ov}, {score, b_sc}, {tki, b_ki}, {tks, b_ks}}, dev);
+    if (dev) (void)hipFree(dev);
+    return rc;
+}
+
+}  // extern "C"

@@ -53,3 +53,28 @@ def all_gather_packed(packed, group=None):
     out = torch.empty((world * packed.shape[0], 4), dtype=packed.dtype, device=packed.device)
     dist.all_gather_into_tensor(out, packed.contiguous(), group=group)
     return out
+
+
+class _DeviceArray:
+    """``__cuda_array_interface__`` view of a device buffer owned by the C-ABI (no copy)."""
+
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {'shape': (n,), 'typestr': typestr, 'data': (int(ptr), False),
+                                         'version': 2}
+
+
+def device_results_packed(batch):
+    """The resident match results of a ``DeviceBatch`` (``dice_batch_result_ptrs``) packed on
+    the device into one int32 [n, 4] torch tensor, ready for the collective -- zero-copy views of
+    the library's buffers, one packing copy on the current stream."""
+    import torch
+    pb, po, ps = batch.result_ptrs()
+    n = batch.n
+    best = torch.as_tensor(_DeviceArray(pb, n, '<i4'), device='cuda')
+    ov = torch.as_tensor(_DeviceArray(po, n, '<i4'), device='cuda')
+    score = torch.as_tensor(_DeviceArray(ps, 2 * n, '<i4'), device='cuda').view(n, 2)
+    out = torch.empty((n, 4), dtype=torch.int32, device='cuda')
+    out[:, 0] = best
+    out[:, 1] = ov
+    out[:, 2:4] = score
+    return out

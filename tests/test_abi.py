@@ -52,6 +52,18 @@ def test_create_rejects_bad_arguments():
     assert lib.dice_create(ctypes.byref(t), 0, ctypes.byref(ctx)) == -1
 
 
+def test_sharded_calls_reject_bad_arguments():
+    lib = _native.load_library()
+    f = _native._Files(0, None, None, None, None)
+    assert lib.dice_match_sharded(None, 1, ctypes.byref(f), 98.0, 0, None, None, None) == -1
+    ctxs = (ctypes.c_void_p * 1)(None)
+    assert lib.dice_match_sharded(ctxs, 0, ctypes.byref(f), 98.0, 0, None, None, None) == -1
+    assert lib.dice_match_sharded(ctxs, 1, ctypes.byref(f), 98.0, 0, None, None, None) == -1
+    assert b'NULL ctx' in lib.dice_last_error()
+    assert lib.dice_similarity_matrix_sharded(ctxs, 1, ctypes.byref(f), 7, None, None, 0, None, None) == -1
+    assert b'gather_mode' in lib.dice_last_error()
+
+
 def test_no_cpu_fallback_without_gpu():
     """On a machine without a gfx950 device the product fails loudly (DICE_E_DEVICE)."""
     import torch

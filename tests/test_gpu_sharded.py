@@ -1,0 +1,131 @@
+"""Multi-device Dice through the C-ABI (dice_match_sharded / dice_similarity_matrix_sharded)
+and the one-process-per-GPU path under torch.distributed.run.
+
+On the one-GPU box the shards' contexts share device 0 (each still has its own host thread,
+stream and resident templates); results must be bit-identical to the single-context calls,
+for both gathers (host slices; device buffer on ctxs[0]'s device + one D2H), for 1-3 shards,
+and with more shards than files. The torchrun test runs the HIP scorer at world size 1 with
+the RCCL all-gather of device-packed results and checks it against the C oracle.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from licensee_amd.license import License
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _scorers(corpus, n):
+    from licensee_amd._native import Scorer
+    return [Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
+                   corpus.is_cc, corpus.n_vocab, device=0) for _ in range(n)]
+
+
+def _sub(fb, n):
+    from licensee_amd._native import FileBatch
+    return FileBatch(fb.bits[:n], fb.wordset_size[:n], fb.length[:n], fb.cc_false_positive[:n])
+
+
+@pytest.fixture(scope='module')
+def vendored():
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    fb = SyntheticCorpus(corpus).generate(0, 100_003, seed=31, nthreads=16)
+    scs = _scorers(corpus, 3)
+    yield corpus, fb, scs
+    for s in scs:
+        s.close()
+
+
+@pytest.mark.parametrize('gather', [0, 1])
+def test_match_sharded_equals_single(vendored, gather):
+    from licensee_amd._native import match_sharded
+    corpus, fb, scs = vendored
+    ref = scs[0].match(fb, 98.0)
+    for n_ctx in (1, 2, 3):
+        got = match_sharded(scs[:n_ctx], fb, 98.0, gather)
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b), (n_ctx, gather)
+    tiny = _sub(fb, 2)                       # more shards than files: empty shards
+    got = match_sharded(scs, tiny, 98.0, gather)
+    for a, b in zip(got, scs[1].match(tiny, 98.0)):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize('gather', [0, 1])
+def test_matrix_sharded_equals_single(vendored, gather):
+    from licensee_amd._native import matrix_sharded
+    corpus, fb, scs = vendored
+    part = _sub(fb, 20_011)
+    for k in (0, 3, 16):
+        ref = scs[0].matrix(part, k)
+        got = matrix_sharded(scs, part, k, gather)
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b), (k, gather)
+
+
+def test_sharded_large_corpus_lds():
+    from licensee_amd._native import match_sharded, matrix_sharded
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    from licensee_amd.synth_templates import synthetic_templates
+    corpus = TemplateCorpus(synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=5))
+    fb = SyntheticCorpus(corpus).generate(0, 30_001, seed=13, nthreads=16)
+    scs = _scorers(corpus, 2)
+    assert scs[0].info()[2] == 2
+    ref = scs[0].match(fb, 98.0)
+    for gather in (0, 1):
+        for a, b in zip(match_sharded(scs, fb, 98.0, gather), ref):
+            assert np.array_equal(a, b)
+    part = _sub(fb, 3001)
+    for a, b in zip(matrix_sharded(scs, part, 4, 1), scs[1].matrix(part, 4)):
+        assert np.array_equal(a, b)
+    for s in scs:
+        s.close()
+
+
+def test_sharded_rejects_mismatched_corpora(vendored):
+    from licensee_amd._native import DiceError, match_sharded
+    from licensee_amd.corpus import TemplateCorpus
+    corpus, fb, scs = vendored
+    small = TemplateCorpus(License.all(hidden=True, pseudo=False)[:5])
+    other = _scorers(small, 1)[0]
+    with pytest.raises(DiceError, match='different corpora'):
+        match_sharded([scs[0], other], _sub(fb, 10), 98.0)
+    other.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_torchrun_world1_hip_scorer_rccl_gather(tmp_path):
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.shard import unpack_results
+    from licensee_amd.synth import SyntheticCorpus
+    from oracle.native import OracleScorer
+    out = str(tmp_path / 'gathered.npy')
+    n_per = 50_000
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
+           '--master-addr=127.0.0.1', f'--master-port={_free_port()}',
+           os.path.join(ROOT, 'tests', 'dist_gpu_worker.py'), out, str(n_per)]
+    subprocess.run(cmd, check=True, env=env, timeout=240, cwd=ROOT)
+    b, o, s = unpack_results(np.load(out))
+    corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    fb = SyntheticCorpus(corpus).generate(0, n_per, seed=7, nthreads=16)
+    orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                       corpus.length, corpus.is_cc, corpus.n_vocab)
+    eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=16, mode=0)
+    assert np.array_equal(b, eb) and np.array_equal(o, eo) and np.array_equal(s, es)
