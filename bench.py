@@ -39,9 +39,9 @@ sys.path.insert(0, ROOT)
 METRIC = 'license files scored/sec (whole node) vs all templates; % HBM roofline'
 HBM_PEAK_GBS = 8000.0
 DEFAULT_FILES = {2: 1_000_000, 3: 1_250_000, 4: 1_000_000, 5: 1_000_000}
-KERNELS = ['dense', 'sparse-program', 'lds-sparse']
+KERNELS = ['dense', 'sparse-program', 'lds-records', 'postings']
 WORKLOADS = {2: 'config2: synthetic perturbed LICENSE files x 47 choosealicense.com templates, Dice#match thr 98',
-             3: 'config3: synthetic files x ~600 synthetic templates (LDS-tiled sparse kernel), one GPU shard '
+             3: 'config3: synthetic files x ~600 synthetic templates (postings kernel), one GPU shard '
                 'of the 10M-file node run',
              4: 'config4: long/mixed COPYING files (2-6 templates + notices) x 47 templates',
              5: 'config5: full N x T similarity matrix + top-k x 47 templates'}

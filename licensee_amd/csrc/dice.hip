@@ -154,39 +154,6 @@ __global__ __launch_bounds__(256) void dice_dense_match(
     }
 }
 
-// Top-k over KM register slots, sorted best-first: rank-and-shift insertion with selects only
-// (p = slots strictly outranking the candidate; a later template goes before equal-scored
-// earlier ones, dice.rb:39). Slots past the caller's k hold lower-ranked valid entries.
-template <int KM>
-struct TopK {
-    int32_t idx[KM];
-    uint32_t ov[KM];
-    int32_t den[KM];
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int j = 0; j < KM; ++j) { idx[j] = -1; ov[j] = 0; den[j] = 1; }
-    }
-    __device__ __forceinline__ void offer(int32_t t, uint32_t o, int32_t d) {
-        int p = 0;
-#pragma unroll
-        for (int j = 0; j < KM; ++j) p += (idx[j] >= 0 && !dice_ge(o, d, ov[j], den[j])) ? 1 : 0;
-#pragma unroll
-        for (int j = KM - 1; j > 0; --j) {
-            const bool mv = j > p;
-            idx[j] = mv ? idx[j - 1] : idx[j];
-            ov[j] = mv ? ov[j - 1] : ov[j];
-            den[j] = mv ? den[j - 1] : den[j];
-        }
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            const bool put = j == p;
-            idx[j] = put ? t : idx[j];
-            ov[j] = put ? o : ov[j];
-            den[j] = put ? d : den[j];
-        }
-    }
-};
-
 template <int TT, int KM>
 __global__ __launch_bounds__(256) void dice_dense_matrix(
     const uint4* __restrict__ files, int64_t n, int32_t wq, const uint4* __restrict__ tq,
@@ -315,7 +282,7 @@ static void ctx_free(dice_ctx* c) {
     if (c->scratch) dice_batch_destroy(c->scratch);
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
-    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt};
+    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_pdm, c->d_ptc};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -376,10 +343,16 @@ int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
     // Sparse-program kernel for small corpora (see dice_program.h).
     rc = dice::program_setup(c, t);  // selects kind 1 when T <= kProgramMaxTemplates
     if (rc == DICE_OK && c->kind == 0 && c->T > kProgramMaxTemplates) {
-        // LDS-tiled sparse kernel for large corpora (dice_lds.hip); DICE_FORCE_DENSE=1 keeps
-        // the dense kernel (A/B and tests).
+        // Large corpora: the postings kernel (dice_post.hip) where its LDS budget allows, else
+        // the LDS-tiled record kernel (dice_lds.hip). DICE_LARGE_KERNEL=lds|post|dense picks one
+        // (A/B and tests); DICE_FORCE_DENSE=1 keeps the dense kernel.
         const char* force = getenv("DICE_FORCE_DENSE");
-        if (!(force && *force == '1')) rc = dice::lds_setup(c, t);
+        const char* pick = getenv("DICE_LARGE_KERNEL");
+        const std::string want = pick && *pick ? pick : "post";
+        if (!(force && *force == '1') && want != "dense") {
+            if (want == "post" && dice::post_feasible(t)) rc = dice::post_setup(c, t);
+            else rc = dice::lds_setup(c, t);
+        }
     }
     if (rc != DICE_OK) {
         ctx_free(c);
@@ -400,7 +373,9 @@ int dice_ctx_info(const dice_ctx* ctx, int32_t* T, int32_t* V, int32_t* kind, in
     if (T) *T = ctx->T;
     if (V) *V = ctx->V;
     if (kind) *kind = ctx->kind;
-    if (entries) *entries = ctx->kind == 2 ? (int32_t)ctx->lds_entries : (int32_t)ctx->prog.entries();
+    if (entries)
+        *entries = ctx->kind == 2 ? (int32_t)ctx->lds_entries
+                 : ctx->kind == 3 ? (int32_t)ctx->post_rows : (int32_t)ctx->prog.entries();
     return DICE_OK;
 }
 
@@ -463,6 +438,7 @@ int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
         HIP_TRY(hipMemsetAsync(b->d_len + n, 0, (size_t)(npad - n) * 4, s));
         HIP_TRY(hipMemsetAsync(b->d_cc + n, 0, (size_t)(npad - n), s));
     }
+    if (c->kind == 3) return DICE_OK;   // the postings kernel reads the row-major bitsets
     const int64_t total = n_tiles * c->wq * kWave;
     const unsigned grid = (unsigned)((total + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(dice_pack_tiles, dim3(grid), dim3(kBlock), 0, s, b->d_rows, n, c->w64, c->wq,
@@ -484,6 +460,9 @@ int dice_batch_match(dice_batch* b, double thr, void* stream) {
         if (rc != DICE_OK) return rc;
     } else if (c->kind == 2) {
         int rc = dice::lds_launch_match(c, b, thr, s);
+        if (rc != DICE_OK) return rc;
+    } else if (c->kind == 3) {
+        int rc = dice::post_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
@@ -524,8 +503,12 @@ int dice_batch_matrix(dice_batch* b, int32_t k, void* stream) {
     hipStream_t s = pick_stream(c, stream);
     const int64_t n_tiles = (b->n + kWave - 1) / kWave;
     const unsigned grid = (unsigned)((n_tiles + (kBlock / kWave) - 1) / (kBlock / kWave));
+    b->mat_rowmajor = c->kind == 3;
     if (c->kind == 1) {
         rc = dice::program_launch_matrix(c, b, k, s);
+        if (rc != DICE_OK) return rc;
+    } else if (c->kind == 3) {
+        rc = dice::post_launch_matrix(c, b, k, s);
         if (rc != DICE_OK) return rc;
     } else {
         if (k <= 4)
@@ -564,6 +547,14 @@ int download_matrix_to(dice_batch* b, uint32_t* ov, double* score, int32_t* tki,
     if (n && !b->d_mov) return fail(DICE_E_STATE, "dice_batch_matrix was not run");
     if (!n) return DICE_OK;
     int rc;
+    if (b->mat_rowmajor) {   // already [n][T] / [n][k]
+        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_mov, (size_t)n * c->T * 4, kind, s));
+        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_mscore, (size_t)n * c->T * 8, kind, s));
+        if (tki && b->k_used) HIP_TRY(hipMemcpyAsync(tki, b->d_tki, (size_t)n * b->k_used * 4, kind, s));
+        if (tks && b->k_used) HIP_TRY(hipMemcpyAsync(tks, b->d_tks, (size_t)n * b->k_used * 8, kind, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return DICE_OK;
+    }
     if (ov && (rc = transpose_to<uint32_t>(b, b->d_mov, c->T, n, ov, s, kind))) return rc;
     if (score && (rc = transpose_to<double>(b, b->d_mscore, c->T, n, score, s, kind))) return rc;
     if (tki && b->k_used && (rc = transpose_to<int32_t>(b, b->d_tki, b->k_used, n, tki, s, kind))) return rc;

@@ -58,4 +58,46 @@ struct Best {
     }
 };
 
+// Candidate a outranks b in the final order: higher score, or equal score and later key
+// (a strict total order over distinct templates: any reduction order gives the same winner).
+__device__ __forceinline__ bool outranks(int32_t ai, uint32_t ao, int32_t ad, int32_t bi, uint32_t bo, int32_t bd) {
+    if (ai < 0) return false;
+    if (bi < 0) return true;
+    const bool ge = dice_ge(ao, ad, bo, bd), le = dice_ge(bo, bd, ao, ad);
+    return ge && (!le || ai > bi);
+}
+
+// Top-k over KM register slots, sorted best-first: rank-and-shift insertion with selects only
+// (p = slots strictly outranking the candidate; a later template goes before equal-scored
+// earlier ones, dice.rb:39). Slots past the caller's k hold lower-ranked valid entries.
+template <int KM>
+struct TopK {
+    int32_t idx[KM];
+    uint32_t ov[KM];
+    int32_t den[KM];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) { idx[j] = -1; ov[j] = 0; den[j] = 1; }
+    }
+    __device__ __forceinline__ void offer(int32_t t, uint32_t o, int32_t d) {
+        int p = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) p += (idx[j] >= 0 && !dice_ge(o, d, ov[j], den[j])) ? 1 : 0;
+#pragma unroll
+        for (int j = KM - 1; j > 0; --j) {
+            const bool mv = j > p;
+            idx[j] = mv ? idx[j - 1] : idx[j];
+            ov[j] = mv ? ov[j - 1] : ov[j];
+            den[j] = mv ? den[j - 1] : den[j];
+        }
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const bool put = j == p;
+            idx[j] = put ? t : idx[j];
+            ov[j] = put ? o : ov[j];
+            den[j] = put ? d : den[j];
+        }
+    }
+};
+
 }  // namespace dice

@@ -37,7 +37,7 @@ struct dice_ctx {
     hipStream_t stream = nullptr;
     uint4* d_tq = nullptr;  // [wq][tpad] template quads (dense kernel)
     int4* d_tc = nullptr;   // [tpad] TplConst (dense kernel)
-    int32_t kind = 0;       // 0 dense, 1 sparse program, 2 LDS-tiled sparse (T > 64)
+    int32_t kind = 0;       // 0 dense, 1 sparse program, 2 LDS-tiled records, 3 postings (T > 64)
     dice::Program prog;     // sparse program (kind 1)
     hipModule_t module = nullptr;
     hipFunction_t prog_match = nullptr;
@@ -51,11 +51,22 @@ struct dice_ctx {
     void* d_lwt = nullptr;
     int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1, lds_wide = 0, lds_tiles = 2;
     int64_t lds_entries = 0;
+    // kind 3 plan (dice_post.hip): postings rows of the narrow words, dense-prefix masks
+    void* d_pwrow = nullptr;   // [64*w64 + 1] u32 first postings row of every word
+    void* d_prow = nullptr;    // [rows][16] u16 template ids (0xFFFF padding)
+    void* d_pdm = nullptr;     // [T][16] u64 dense-prefix masks
+    void* d_ptc = nullptr;     // [T] int4 template constants
+    int32_t post_dense = 0, post_tpad = 0;
+    int64_t post_rows = 0;
 };
 
 namespace dice {
 int lds_setup(dice_ctx* c, const dice_templates* t);
 int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+bool post_feasible(const dice_templates* t);
+int post_setup(dice_ctx* c, const dice_templates* t);
+int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s);
 // the ctx's reusable batch for the host-buffer calls (grown on demand)
 int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out);
 // result downloads to host memory or (kind hipMemcpyDefault) another device's memory;
@@ -81,6 +92,7 @@ struct dice_batch {
     int64_t mat_cap = 0;
     int32_t mat_k = 0;
     int32_t k_used = 0;
+    bool mat_rowmajor = false;      // kind 3 writes [n][T] / [n][k] directly (no transpose)
     uint32_t* d_mov = nullptr;      // template-major [T][capacity] (coalesced stores)
     double* d_mscore = nullptr;     // template-major [T][capacity]
     int32_t* d_tki = nullptr;

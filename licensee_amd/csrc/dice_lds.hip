@@ -128,14 +128,6 @@ __device__ __forceinline__ void ring_enter(int32_t p, int32_t nchunk, const uint
     }
 }
 
-// Candidate a outranks b in the final order: higher score, or equal score and later key.
-__device__ __forceinline__ bool outranks(int32_t ai, uint32_t ao, int32_t ad, int32_t bi, uint32_t bo, int32_t bd) {
-    if (ai < 0) return false;
-    if (bi < 0) return true;
-    const bool ge = dice_ge(ao, ad, bo, bd), le = dice_ge(bo, bd, ao, ad);
-    return ge && (!le || ai > bi);
-}
-
 template <int G, int kTiles, bool kWide>
 __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
     const uint4* __restrict__ tiles, int64_t n, int32_t wq, int32_t nslab, int32_t T,

@@ -6,9 +6,10 @@
     files (match, full matrix, top-k), then 1M files (the bench size) through size-independent
     properties: two launches bit-identical, match == thresholded top-1 of the matrix kernel,
     top-k sorted and consistent with the matrix rows, CC filter, and a 20k oracle sample.
-  * config 3 -- one GPU's shard of the 10M x ~600-template run (1.25M files, LDS-tiled kernel):
-    two launches bit-identical (the LDS kernel's asm-wait convention, dice_lds.hip:54-66), a 20k
-    oracle sample in hash mode, and the match/matrix top-1 agreement on 50k files.
+  * config 3 -- one GPU's shard of the 10M x ~600-template run (1.25M files), postings kernel
+    (default) and LDS record kernel: two launches bit-identical (for the LDS kernel also its
+    asm-wait convention, dice_lds.hip:54-66), a 20k oracle sample in hash mode, and the
+    match/matrix top-1 agreement on 50k files.
 """
 import numpy as np
 import pytest
@@ -102,16 +103,19 @@ def test_config4_full_size_properties(vendored):
     sc.close()
 
 
-def test_config3_shard_lds(monkeypatch):
+@pytest.mark.parametrize('kernel', ['post', 'lds'])
+def test_config3_shard(kernel, monkeypatch):
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
     from licensee_amd.synth_templates import synthetic_templates
-    for k in ('DICE_FORCE_DENSE', 'DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_LDS_G'):
+    for k in ('DICE_FORCE_DENSE', 'DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_LDS_G',
+              'DICE_POST_DENSE'):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv('DICE_LARGE_KERNEL', kernel)
     corpus = TemplateCorpus(synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=20250202))
     fb = SyntheticCorpus(corpus).generate(0, 1_250_000, seed=20250202, nthreads=16)
     sc = _scorer(corpus)
-    assert sc.info()[2] == 2
+    assert sc.info()[2] == {'lds': 2, 'post': 3}[kernel]
     batch = sc.batch(fb.n)
     batch.upload(fb)
     batch.match(98.0)

@@ -1,5 +1,6 @@
 """GPU parity across corpus shapes: template counts either side of the sparse-program limit
-(64), of the dense kernel's 48-template tile and of the LDS kernel's one-pass capacity (640),
+(64), of the dense kernel's 48-template tile, of the LDS kernel's one-pass capacity (640) and of
+the postings kernel's 64-template lane rounds (65, 97, 130, 700),
 tiny vocabularies (one 128-bit quad), every kernel where it applies. Bit-exact against the C oracle (oracle/dice_ref.c) for
 match (keys, overlaps, scores with ==) and the full similarity matrix + top-k.
 """
@@ -24,13 +25,22 @@ def corpus_of(n):
     return synthetic_templates(real, n, seed=n)
 
 
-KIND = {'dense': 0, 'program': 1, 'lds': 2}
+KIND = {'dense': 0, 'program': 1, 'lds': 2, 'post': 3}
 
 
-# every kernel where it applies: the sparse program serves T <= 64, the LDS kernel T > 64,
-# the dense kernel (DICE_FORCE_DENSE) any T
-CASES = [(n, k) for n in SIZES for k in ('program', 'lds', 'dense')
-         if not (k == 'program' and n > 64) and not (k == 'lds' and n <= 64)]
+# every kernel where it applies: the sparse program serves T <= 64, the postings kernel
+# (default) and the LDS record kernel T > 64, the dense kernel (DICE_FORCE_DENSE) any T
+CASES = [(n, k) for n in SIZES for k in ('program', 'lds', 'post', 'dense')
+         if not (k == 'program' and n > 64) and not (k in ('lds', 'post') and n <= 64)]
+
+
+def select_kernel(monkeypatch, kernel):
+    monkeypatch.delenv('DICE_POST_DENSE', raising=False)
+    if kernel == 'dense':
+        monkeypatch.setenv('DICE_FORCE_DENSE', '1')
+    else:
+        monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
+    monkeypatch.setenv('DICE_LARGE_KERNEL', 'lds' if kernel == 'lds' else 'post')
 
 
 @pytest.mark.parametrize('n_templates,kernel', CASES)
@@ -39,10 +49,7 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
     from oracle.native import OracleScorer
-    if kernel == 'dense':
-        monkeypatch.setenv('DICE_FORCE_DENSE', '1')
-    else:
-        monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
+    select_kernel(monkeypatch, kernel)
     c = TemplateCorpus(corpus_of(n_templates))
     fb = SyntheticCorpus(c).generate(0, 2000, seed=n_templates, nthreads=8)
     sc = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab, device=0)
@@ -69,14 +76,17 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
         sc.close()
 
 
-@pytest.mark.parametrize('tiles', [2, 4])
+@pytest.mark.parametrize('tiles', [2, 4, 'post'])
 @pytest.mark.parametrize('n_files', [0, 1, 63, 150, 1000])
 def test_lds_ragged_batches(n_files, tiles, monkeypatch):
     """LDS kernel (T = 130) on batches that end mid-tile and mid-group: a workgroup holds 2 (or, as
     the DICE_LDS_TILES=4 A/B layout, 4) tiles of 64 files, so 150 files leave a partial group and a
-    22-file tail; 0 files launch nothing."""
-    monkeypatch.setenv('DICE_LDS_TILES', str(tiles))
-    monkeypatch.setenv('DICE_LDS_G', '16' if tiles == 2 else '12')
+    22-file tail; 0 files launch nothing. The postings kernel ('post', one 64-file tile per
+    workgroup) on the same batches."""
+    kernel = 'post' if tiles == 'post' else 'lds'
+    monkeypatch.setenv('DICE_LARGE_KERNEL', kernel)
+    monkeypatch.setenv('DICE_LDS_TILES', str(tiles if tiles != 'post' else 2))
+    monkeypatch.setenv('DICE_LDS_G', '12' if tiles == 4 else '16')
     from licensee_amd._native import FileBatch, Scorer
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
@@ -87,7 +97,7 @@ def test_lds_ragged_batches(n_files, tiles, monkeypatch):
     fb = FileBatch(fb.bits[:n_files], fb.wordset_size[:n_files], fb.length[:n_files], fb.cc_false_positive[:n_files])
     sc = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab, device=0)
     try:
-        assert sc.info()[2] == KIND['lds']
+        assert sc.info()[2] == KIND[kernel]
         orc = OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
         best, ov, score = sc.match(fb, 98.0)
         assert best.shape == ov.shape == score.shape == (n_files,)
@@ -95,5 +105,9 @@ def test_lds_ragged_batches(n_files, tiles, monkeypatch):
             return
         eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=8)
         assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+        mov, msc, tki, tks = sc.matrix(fb, 3)
+        emov, emsc = orc.matrix(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, nthreads=8)
+        assert np.array_equal(mov, emov) and np.array_equal(msc, emsc)
+        assert np.array_equal(tks[:, 0], score)
     finally:
         sc.close()

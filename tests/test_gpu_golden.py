@@ -182,7 +182,8 @@ LDS_VARIANTS = {'lds-fwd': {'DICE_LDS_SNAKE': '0'}, 'lds-narrow': {'DICE_LDS_WID
                 'lds-t4': {'DICE_LDS_TILES': '4', 'DICE_LDS_G': '12'}}
 
 
-@pytest.mark.parametrize('kernel', ['lds', 'lds-g12', 'lds-g24', 'lds-fwd', 'lds-narrow', 'lds-t4', 'dense'])
+@pytest.mark.parametrize('kernel', ['post', 'post-d0', 'post-d4', 'post-d16', 'lds', 'lds-g12', 'lds-g24', 'lds-fwd',
+                                    'lds-narrow', 'lds-t4', 'dense'])
 def test_large_corpus_600_templates(kernel, monkeypatch):
     from licensee_amd._native import Scorer
     from licensee_amd.corpus import TemplateCorpus
@@ -198,13 +199,17 @@ def test_large_corpus_600_templates(kernel, monkeypatch):
         monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
     # templates per wave per pass of the LDS kernel: 16 (default, 3 passes here), 12 (4), 24 (2)
     monkeypatch.setenv('DICE_LDS_G', kernel[5:] if kernel.startswith('lds-g') else '16')
-    for k in ('DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES'):
+    for k in ('DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_POST_DENSE'):
         monkeypatch.delenv(k, raising=False)
     for k, v in LDS_VARIANTS.get(kernel, {}).items():
         monkeypatch.setenv(k, v)
+    # postings kernel: cost-model dense prefix, or forced to 0 / 4 / 16 u64 words
+    monkeypatch.setenv('DICE_LARGE_KERNEL', 'post' if kernel.startswith('post') else 'lds')
+    if kernel.startswith('post-d'):
+        monkeypatch.setenv('DICE_POST_DENSE', kernel[6:])
     sc = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
                 corpus.is_cc, corpus.n_vocab, device=0)
-    assert sc.info()[2] == (0 if kernel == 'dense' else 2)
+    assert sc.info()[2] == (0 if kernel == 'dense' else 3 if kernel.startswith('post') else 2)
     orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
                        corpus.length, corpus.is_cc, corpus.n_vocab)
     best, ov, score = sc.match(fb, 98.0)
@@ -215,6 +220,10 @@ def test_large_corpus_600_templates(kernel, monkeypatch):
     assert np.array_equal(mov, emov) and np.array_equal(msc, emsc)
     assert np.array_equal(tks[:, 0], score)
     assert np.array_equal(np.where(tks[:, 0] >= 98.0, tki[:, 0], -1), best)
+    rows = np.arange(fb.n)
+    for j in range(5):
+        assert np.array_equal(msc[rows, tki[:, j]], tks[:, j])
+    assert (tks[:, :-1] >= tks[:, 1:]).all()
     sc.close()
 
 

@@ -79,7 +79,7 @@ def test_sharded_large_corpus_lds():
     corpus = TemplateCorpus(synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=5))
     fb = SyntheticCorpus(corpus).generate(0, 30_001, seed=13, nthreads=16)
     scs = _scorers(corpus, 2)
-    assert scs[0].info()[2] == 2
+    assert scs[0].info()[2] in (2, 3)
     ref = scs[0].match(fb, 98.0)
     for gather in (0, 1):
         for a, b in zip(match_sharded(scs, fb, 98.0, gather), ref):

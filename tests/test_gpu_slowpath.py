@@ -89,13 +89,14 @@ def test_sparse_program_corpus_outside_envelope(vendored):
     sc.close()
 
 
-@pytest.mark.parametrize('kernel', ['lds', 'dense'])
+@pytest.mark.parametrize('kernel', ['post', 'lds', 'dense'])
 def test_large_corpus_mixed_lanes(kernel, monkeypatch):
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
     from licensee_amd.synth_templates import synthetic_templates
-    for k in ('DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_LDS_G'):
+    for k in ('DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_LDS_G', 'DICE_POST_DENSE'):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv('DICE_LARGE_KERNEL', 'lds' if kernel == 'lds' else 'post')
     if kernel == 'dense':
         monkeypatch.setenv('DICE_FORCE_DENSE', '1')
     else:
@@ -106,6 +107,6 @@ def test_large_corpus_mixed_lanes(kernel, monkeypatch):
     oc = outside_fast_envelope(corpus)
     for c in (corpus, oc):
         sc = _scorer(c)
-        assert sc.info()[2] == (0 if kernel == 'dense' else 2)
+        assert sc.info()[2] == {'dense': 0, 'lds': 2, 'post': 3}[kernel]
         _check(sc, _oracle(c), fb, c.is_cc, k=4)
         sc.close()
