@@ -282,7 +282,7 @@ static void ctx_free(dice_ctx* c) {
     if (c->scratch) dice_batch_destroy(c->scratch);
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
-    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_pdm, c->d_ptc};
+    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -383,7 +383,7 @@ void dice_batch_destroy(dice_batch* b) {
     if (!b) return;
     DeviceGuard g(b->ctx->device);
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,  b->d_best, b->d_ov,
-                    b->d_score, b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage};
+                    b->d_score, b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;

@@ -52,11 +52,13 @@ struct dice_ctx {
     int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1, lds_wide = 0, lds_tiles = 2;
     int64_t lds_entries = 0;
     // kind 3 plan (dice_post.hip): postings rows of the narrow words, dense-prefix masks
-    void* d_pwrow = nullptr;   // [64*w64 + 1] u32 first postings row of every word
-    void* d_prow = nullptr;    // [rows][16] u16 template ids (0xFFFF padding)
+    void* d_pwrow = nullptr;   // (unused)
+    void* d_prow = nullptr;    // [64*w64][16] u16 postings row per word (short ids / long word ref)
+    void* d_povf = nullptr;    // flat u16 template ids of the long words
     void* d_pdm = nullptr;     // [T][16] u64 dense-prefix masks
     void* d_ptc = nullptr;     // [T] int4 template constants
-    int32_t post_dense = 0, post_tpad = 0;
+    int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0;
+    bool post_fast = false;
     int64_t post_rows = 0;
 };
 
@@ -98,5 +100,7 @@ struct dice_batch {
     int32_t* d_tki = nullptr;
     double* d_tks = nullptr;
     void* d_stage = nullptr;        // row-major staging for downloads
+    void* d_pdense = nullptr;       // kind 3: dense-prefix partial overlaps [capacity][tp] u16
+    size_t pdense_bytes = 0;
     size_t stage_bytes = 0;
 };

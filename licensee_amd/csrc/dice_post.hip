@@ -39,144 +39,352 @@ namespace dice {
 
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
-constexpr int kPostMaxTpad = 768;        // LDS budget of the counter matrix
+constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
 constexpr int kPostMaxDense = 16;        // dense prefix u64 words
 constexpr int kRowW = 16;                // template ids per postings row
-constexpr int kWordCap = 192;            // per-wave queue of (row start, rows)
-constexpr uint16_t kNoTpl = 0xFFFF;
+constexpr int kWordCap = 256;            // per-wave queue of narrow word ids
+constexpr int kMidCap = 128;             // per-wave queue of words with 9-16 postings
+constexpr uint16_t kNoTpl = 0xFFFF;      // empty row entry
+constexpr uint16_t kMore = 0xFFFE;       // row entry 15: a long word (entries 0-1 offset, 2 length)
+constexpr int kLongCap = 128;            // per-wave queue of long words (offset, length)
+constexpr int kChunks = 3;               // 64-word chunks of a file loaded together
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// "a ranks at or above b" in score order. FAST: both overlaps < 2^11 and both denominators in
+// [1, 2^21) with scores < 1024 (the file and corpus envelope checked by the caller), where
+// the rational compare is exact in 24-bit multiplies and equals the double order (dice_common.h).
+template <bool FAST>
+__device__ __forceinline__ bool ge(uint32_t oa, int32_t da, uint32_t ob, int32_t db) {
+    if (FAST) return __umul24(oa, (uint32_t)db) >= __umul24(ob, (uint32_t)da);
+    return dice_ge(oa, da, ob, db);
+}
+
+template <bool FAST>
+__device__ __forceinline__ bool outranks_t(int32_t ai, uint32_t ao, int32_t ad, int32_t bi, uint32_t bo, int32_t bd) {
+    if (ai < 0) return false;
+    if (bi < 0) return true;
+    const bool g = ge<FAST>(ao, ad, bo, bd), l = ge<FAST>(bo, bd, ao, ad);
+    return g && (!l || ai > bi);
+}
+
 // Wave-wide argmax of (idx, ov, den) under `outranks` (butterfly over all 64 lanes).
+template <bool FAST = false>
 __device__ __forceinline__ void wave_best(int32_t& bi, uint32_t& bo, int32_t& bd) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
         const int32_t oi = __shfl_xor(bi, m);
         const uint32_t oo = (uint32_t)__shfl_xor((int)bo, m);
         const int32_t od = __shfl_xor(bd, m);
-        if (outranks(oi, oo, od, bi, bo, bd)) { bi = oi; bo = oo; bd = od; }
+        if (outranks_t<FAST>(oi, oo, od, bi, bo, bd)) { bi = oi; bo = oo; bd = od; }
     }
 }
 
-template <bool kMatrix, int KM>
-__global__ __launch_bounds__(kPostWaves * kWave) void dice_post_kernel(
-    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tpad,
-    const uint64_t* __restrict__ dmask, const uint32_t* __restrict__ wrow, const uint16_t* __restrict__ prow,
-    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
-    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
-    double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks) {
-    constexpr int kStrideMax = kPostMaxTpad + 2;
-    __shared__ uint32_t cnt32[kPostFiles * kStrideMax / 2];   // u16 counters, [file][template]
-    __shared__ int4 tcs[kPostMaxTpad];
-    __shared__ uint2 wl[kPostWaves][kWordCap];                 // queued (first row, rows)
-    uint16_t* cnt16 = reinterpret_cast<uint16_t*>(cnt32);
-    // row stride tpad + 2 halves = 32m + 1 dwords: lanes = files (phase 1) hit 64 distinct banks
-    const int32_t cstride = tpad + 2;
+// Inclusive prefix sum over the 64 lanes (DPP: row shifts within each 16-lane row, then the
+// row-15 / row-31 broadcasts); every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
 
+__device__ __forceinline__ uint32_t lane_rank(uint64_t bal) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+}
+
+__device__ __forceinline__ void count(uint32_t* crow32, uint32_t id) {
+    atomicAdd(&crow32[id >> 1], 1u << ((id & 1) * 16));
+}
+
+// Long words (> 16 narrow postings): 64 lanes per word, 4 words' id loads in flight.
+__device__ __forceinline__ void walk_long(const uint2* lq, uint32_t& nl, const uint16_t* __restrict__ plong,
+                                          uint32_t* crow32, int lane) {
+    constexpr int kB = 4;   // words whose id loads are in flight together
+    for (uint32_t e0 = 0; e0 < nl; e0 += kB) {
+        uint16_t id[kB];
+        uint2 q[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            q[u] = e0 + u < nl ? lq[e0 + u] : make_uint2(0, 0);
+            id[u] = lane < (int)q[u].y ? plong[(int64_t)q[u].x + lane] : kNoTpl;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            if (id[u] != kNoTpl) count(crow32, id[u]);
+            for (uint32_t r = kWave; r < q[u].y; r += kWave)   // > 64 postings (rare)
+                if (r + lane < q[u].y) count(crow32, plong[(int64_t)q[u].x + r + lane]);
+        }
+    }
+    nl = 0;
+}
+
+// Second halves (entries 8-15) of the queued MID words (9-16 postings), one lane per word.
+__device__ __forceinline__ void walk_mid(const uint32_t* mq, uint32_t& nm, const uint16_t* __restrict__ prow,
+                                         uint32_t* crow32, int lane) {
+    for (uint32_t e0 = 0; e0 < nm; e0 += kWave) {
+        const uint32_t e = e0 + lane;
+        uint4 r1 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (e < nm) r1 = reinterpret_cast<const uint4*>(prow + (int64_t)mq[e] * kRowW)[1];
+        const uint32_t rr[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t id = (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+            if (id < kMore) count(crow32, id);
+        }
+    }
+    nm = 0;
+}
+
+// Queued narrow words, one lane per word: its 32-byte row in two loads, then the first 8
+// template ids (8 predicated counter adds). Words with more ids wait in the mid queue (ids
+// 8-15) or, past 16, in the long queue; each queue is walked once it holds >= 64 words, so
+// its passes run with (nearly) every lane busy.
+__device__ __forceinline__ void load_rows(const uint32_t* wq, uint32_t nq, uint32_t e0, const uint16_t* __restrict__ prow,
+                                          int lane, uint32_t& w, uint4& r0, uint4& r1) {
+    const uint32_t e = e0 + lane;
+    r0 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    r1 = r0;
+    w = 0;
+    if (e < nq) {
+        w = wq[e];
+        const uint4* rp = reinterpret_cast<const uint4*>(prow + (int64_t)w * kRowW);
+        r0 = rp[0];
+        r1 = rp[1];
+    }
+}
+
+__device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint2* lq, uint32_t& nl, uint32_t* mq,
+                                           uint32_t& nm, const uint16_t* __restrict__ prow,
+                                           const uint16_t* __restrict__ plong, uint32_t* crow32, int lane) {
+    uint32_t w;
+    uint4 r0, r1;
+    if (nq) load_rows(wq, nq, 0, prow, lane, w, r0, r1);
+    for (uint32_t e0 = 0; e0 < nq; e0 += kWave) {
+        // the next pass's rows are requested before this pass's counter adds
+        uint32_t wn = 0;
+        uint4 n0 = r0, n1 = r1;
+        if (e0 + kWave < nq) load_rows(wq, nq, e0 + kWave, prow, lane, wn, n0, n1);
+        const bool lng = (r1.w >> 16) == kMore;
+        const bool mid = !lng && (r1.x & 0xFFFFu) != kNoTpl;
+        const uint64_t bl = __ballot(lng), bm = __ballot(mid);
+        if (bl) {
+            if (lng) lq[nl + lane_rank(bl)] = make_uint2(r0.x, r0.y & 0xFFFFu);   // (offset, length)
+            nl = rfl(nl + (uint32_t)__builtin_popcountll(bl));
+            if (lng) r0 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        }
+        if (bm) {
+            if (mid) mq[nm + lane_rank(bm)] = w;
+            nm = rfl(nm + (uint32_t)__builtin_popcountll(bm));
+        }
+        const uint32_t rr[4] = {r0.x, r0.y, r0.z, r0.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t id = (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+            if (id < kMore) count(crow32, id);
+        }
+        if (nl > kLongCap - kWave) walk_long(lq, nl, plong, crow32, lane);
+        if (nm > kMidCap - kWave) walk_mid(mq, nm, prow, crow32, lane);
+        w = wn;
+        r0 = n0;
+        r1 = n1;
+    }
+}
+
+// Phase 1 (dense prefix, lanes = files): wave w scores templates [w*TW, (w+1)*TW) over the 64
+// files' first D u64 words (DP = D rounded up to a multiple of 4; masks past D are zero). The
+// template masks are wave-uniform scalar loads, the next template's issued before this one is
+// scored. Partial overlaps go to an LDS [file][template] u16 stage (row stride tp + 2 halves:
+// an odd number of dwords, so the 64 lanes hit 64 banks), then out as row-major [n][tp] u16.
+template <int DP, int TPMAX>
+__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_dense(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
+    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ dense) {
+    __shared__ uint32_t stage32[kPostFiles * (TPMAX + 2) / 2];   // <= 78 KiB at TPMAX 608: 2 per CU
+    uint16_t* st = reinterpret_cast<uint16_t*>(stage32);
+    const int32_t cs = tp + 2;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
-
-    for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
-
-    // ---- phase 1: dense prefix, lanes = files --------------------------------------------
     {
         const int64_t file = f0 + lane;
         const bool valid = file < n;
-        uint64_t fd[kPostMaxDense];
+        uint64_t fd[DP];
 #pragma unroll
-        for (int d = 0; d < kPostMaxDense; ++d) fd[d] = (valid && d < D) ? rows[file * w64 + d] : 0;
+        for (int d = 0; d < DP; ++d) fd[d] = (valid && d < D) ? rows[file * w64 + d] : 0;
         const int32_t tw = (T + kPostWaves - 1) / kPostWaves;
         const int32_t tb = wave * tw, te = min(T, tb + tw);
-        uint16_t* crow = cnt16 + lane * cstride;
+        uint16_t* crow = st + lane * cs;
+        // template masks: wave-uniform scalar loads (scalar returns are unordered, so a prefetch
+        // would be waited for with the current template's masks: no software pipelining; the
+        // other waves of the SIMD cover the latency)
         for (int32_t t = tb; t < te; ++t) {
             const uint64_t* m = dmask + (int64_t)t * kPostMaxDense;
-            uint32_t acc = 0;
+            // four independent accumulator chains (a single v_bcnt chain stalls on its latency)
+            uint32_t acc[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int d = 0; d < kPostMaxDense; ++d) {
-                if (d < D) {
-                    const uint64_t md = m[d];
-                    acc += __builtin_popcount((uint32_t)fd[d] & (uint32_t)md) +
-                           __builtin_popcount((uint32_t)(fd[d] >> 32) & (uint32_t)(md >> 32));
-                }
+            for (int d = 0; d < DP; ++d) {
+                const uint64_t md = m[d];
+                acc[(2 * d) & 3] += __builtin_popcount((uint32_t)fd[d] & (uint32_t)md);
+                acc[(2 * d + 1) & 3] += __builtin_popcount((uint32_t)(fd[d] >> 32) & (uint32_t)(md >> 32));
             }
-            crow[t] = (uint16_t)acc;
+            crow[t] = (uint16_t)(acc[0] + acc[1] + acc[2] + acc[3]);
         }
+        for (int32_t t = T + (threadIdx.x >> 6); t < tp; t += kPostWaves) crow[t] = 0;   // row padding
     }
     __syncthreads();
+    for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
+        const int64_t file = f0 + fi;
+        if (file >= n) break;
+        const uint32_t* src = stage32 + (fi * cs) / 2;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(dense + file * tp);
+        for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
+    }
+}
 
-    // ---- phases 2 + 3, one file per wave ----------------------------------------------------
+// Phases 2 + 3, one file per wave (16 waves x 4 files per workgroup). Each wave owns one u16
+// counter row in LDS (zero between files). Narrow words are queued from the file's u64 words
+// >= D and walked (walk_short / walk_mid / walk_long) after the file's dense partials (from
+// dice_post_dense) are added in; scoring reads and re-zeroes the counters and reduces over the
+// wave. The LDS footprint (~74 KiB) and <= 64 VGPRs leave room for two workgroups per CU.
+template <bool kMatrix, int KM>
+__device__ __forceinline__ void post_narrow_body(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
+    const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
+    double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
+    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
+    // diag (DICE_POST_DIAG, diagnostics only -- results are wrong): 2 skips the postings walk,
+    // 4 skips the narrow-word extraction, 8 skips scoring
+    constexpr int kRowMax = kPostMaxTpad + 2;
+    constexpr int kTJ = kPostMaxTpad / kWave;                  // templates per lane
+    __shared__ uint32_t cnt32[kPostWaves * kRowMax / 2];       // u16 counters, one row per wave
+    __shared__ int4 tcs[kPostMaxTpad];
+    __shared__ uint32_t wq[kPostWaves][kWordCap];              // queued narrow word ids
+    __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
+    __shared__ uint32_t mq[kPostWaves][kMidCap];               // queued mid words
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
+    uint32_t* crow32 = cnt32 + wave * (kRowMax / 2);
+    uint16_t* crow = reinterpret_cast<uint16_t*>(crow32);
+    for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
+    for (int i = lane; i < kRowMax / 2; i += kWave) crow32[i] = 0;
+    __syncthreads();
+
+    const int32_t pb0 = (diag & 4) ? w64 : D;
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
         const int64_t file = f0 + fi;
         if (file >= n) break;   // wave-uniform
         const uint64_t* row = rows + file * w64;
-        uint32_t* crow32 = cnt32 + (fi * cstride) / 2;
-        uint32_t nq = 0;        // queued words (uniform)
-
-        // walk queued words: 4 words per pass, 16 lanes per word, one row of 16 ids per lane group
-        auto flush = [&]() {
-            const int g = lane >> 4, sub = lane & 15;
-            for (uint32_t e0 = 0; e0 < nq; e0 += 4) {
-                const uint32_t e = e0 + g;
-                uint2 q = make_uint2(0, 0);
-                if (e < nq) q = wl[wave][e];
-                for (uint32_t r = 0; r < q.y; ++r) {
-                    const uint16_t id = prow[(int64_t)(q.x + r) * kRowW + sub];
-                    if (id != kNoTpl) atomicAdd(&crow32[id >> 1], 1u << ((id & 1) * 16));
-                }
-            }
-            nq = 0;
-        };
-
-        for (int32_t pb = D; pb < w64; pb += kWave) {
-            const int32_t p = pb + lane;
-            uint64_t x = p < w64 ? row[p] : 0;
-            while (__any(x != 0)) {
-                const bool has = x != 0;
-                const int b = has ? __builtin_ctzll(x) : 0;
-                x &= x - 1;
-                const int64_t w = (int64_t)p * 64 + b;
-                uint32_t r0 = 0, nr = 0;
-                if (has) {
-                    r0 = wrow[w];
-                    nr = wrow[w + 1] - r0;
-                }
-                const bool put = nr != 0;
-                const uint64_t bal = __ballot(put);
-                const uint32_t pos = nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-                if (put) wl[wave][pos] = make_uint2(r0, nr);
-                nq += (uint32_t)__builtin_popcountll(bal);
-                if (nq > kWordCap - kWave) flush();
+        // this file's dense partials start its counter row (a plain copy of u16 pairs: the row is
+        // zero here and this wave's postings adds come after it; no registers held across the walk)
+        {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + file * tp);
+#pragma unroll
+            for (int j = 0; j < (kPostMaxTpad / 2 + kWave - 1) / kWave; ++j) {
+                const int32_t i = lane + j * kWave;
+                if (i < tp / 2) crow32[i] = src[i];
             }
         }
-        flush();
-
-        // ---- phase 3: score, lanes = templates -------------------------------------------------
         const uint32_t wf = wfp[file];
         const int32_t lf = lenp[file];
         const bool cc = ccp[file] != 0;
-        const uint16_t* crow = cnt16 + fi * cstride;
+        uint32_t nq = 0;           // queued narrow words (wave-uniform)
+        uint32_t nl = 0, nm = 0;   // queued long / mid words (uniform)
+
+        // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
+        // together. Per chunk a wave prefix sum of the lanes' bit counts gives every lane its
+        // queue slots, and each lane writes its own words (a chunk of more than kWordCap words
+        // -- a file holding most of the vocabulary -- goes round by round instead).
+        for (int32_t pb = pb0; pb < w64; pb += kChunks * kWave) {
+            uint64_t xs[kChunks];
+#pragma unroll
+            for (int c = 0; c < kChunks; ++c) {
+                const int32_t p = pb + c * kWave + lane;
+                xs[c] = p < w64 ? row[p] : 0;
+            }
+#pragma unroll
+            for (int c = 0; c < kChunks; ++c) {
+                const uint32_t wbase = (uint32_t)(pb + c * kWave + lane) * 64u;
+                uint64_t x = xs[c];
+                const uint32_t cnt = (uint32_t)__builtin_popcountll(x);
+                const uint32_t incl = wave_incl_scan(cnt);
+                const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
+                if (total == 0) continue;
+                if (nq + total > kWordCap) {
+                    if (!(diag & 2)) walk_short(wq[wave], nq, lq[wave], nl, mq[wave], nm, prow, plong, crow32, lane);
+                    nq = 0;
+                }
+                if (total <= kWordCap) {
+                    uint32_t pos = nq + incl - cnt;
+                    while (x) {
+                        wq[wave][pos++] = wbase + (uint32_t)__builtin_ctzll(x);
+                        x &= x - 1;
+                    }
+                    nq += total;
+                    continue;
+                }
+                while (__any(x != 0)) {
+                    const bool has = x != 0;
+                    const uint32_t w = wbase + (has ? (uint32_t)__builtin_ctzll(x) : 0u);
+                    x &= x - 1;
+                    const uint64_t bal = __ballot(has);
+                    if (has) wq[wave][nq + lane_rank(bal)] = w;
+                    nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
+                    if (nq > kWordCap - kWave) {
+                        if (!(diag & 2)) walk_short(wq[wave], nq, lq[wave], nl, mq[wave], nm, prow, plong, crow32, lane);
+                        nq = 0;
+                    }
+                }
+            }
+        }
+        if (!(diag & 2)) walk_short(wq[wave], nq, lq[wave], nl, mq[wave], nm, prow, plong, crow32, lane);
+        walk_long(lq[wave], nl, plong, crow32, lane);
+        walk_mid(mq[wave], nm, prow, crow32, lane);
+
+        // ---- phase 3: score, lanes = templates (t = lane + 64 j) ------------------------------
+        if (diag & 8) {
+#pragma unroll
+            for (int j = 0; j < kTJ; ++j)
+                if (lane + j * kWave < T) crow[lane + j * kWave] = 0;
+            continue;
+        }
         int32_t bi = -1, bd = 1;
         uint32_t bo = 0;
         TopK<KM> top;
         if (kMatrix) top.init();
-        for (int32_t t = lane; t < T; t += kWave) {
-            const uint32_t ov = crow[t];
-            const int4 c = tcs[t];
-            const int32_t den = dice_den(c, wf, lf);
-            if (kMatrix) {
-                mov[file * T + t] = ov;
-                msc[file * T + t] = dice_score(ov, den);
-            }
-            if (!(c.w && cc)) {
-                if (kMatrix) top.offer(t, ov, den);
-                else if (bi < 0 || dice_ge(ov, den, bo, bd)) { bi = t; bo = ov; bd = den; }
+        // file inside the fast envelope (wave-uniform): 24-bit exact compares
+        const bool fast = corpus_fast && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
+#pragma unroll
+        for (int j = 0; j < kTJ; ++j) {
+            const int32_t t = lane + j * kWave;
+            if (t < T) {
+                const uint32_t ov = crow[t];
+                crow[t] = 0;
+                const int4 c = tcs[t];
+                const int32_t den = dice_den(c, wf, lf);
+                if (kMatrix) {
+                    mov[file * T + t] = ov;
+                    msc[file * T + t] = dice_score(ov, den);
+                }
+                if (!(c.w && cc)) {
+                    if (kMatrix) top.offer(t, ov, den);
+                    else if (bi < 0 || (fast ? ge<true>(ov, den, bo, bd) : ge<false>(ov, den, bo, bd))) {
+                        bi = t;
+                        bo = ov;
+                        bd = den;
+                    }
+                }
             }
         }
         if (!kMatrix) {
-            wave_best(bi, bo, bd);
+            if (fast) wave_best<true>(bi, bo, bd);
+            else wave_best<false>(bi, bo, bd);
             if (lane == 0) {
                 const double s = bi >= 0 ? dice_score(bo, bd) : 0.0;
                 best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
@@ -203,6 +411,31 @@ __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_kernel(
             }
         }
     }
+}
+
+// Match mode held to 64 VGPRs (8 waves per SIMD: two workgroups per CU); the matrix mode's
+// top-k slots need more registers and run at the occupancy they get.
+__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_narrow_match(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
+    const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
+    double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
+    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
+    post_narrow_body<false, 1>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+                               score_out, k, mov, msc, tki, tks, diag, corpus_fast);
+}
+
+template <int KM>
+__global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
+    const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
+    double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
+    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
+    post_narrow_body<true, KM>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+                               score_out, k, mov, msc, tki, tks, diag, false);
 }
 
 // ---- host side ---------------------------------------------------------------------------
@@ -248,23 +481,35 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     }
     std::vector<int64_t> sq((size_t)w64, 0);
     for (int64_t w = 0; w < nbits; ++w) sq[(size_t)(w / 64)] += (int64_t)plen[(size_t)w] * plen[(size_t)w];
-    const int D = pick_dense(sq, T, w64);
-    // postings rows of the narrow words (u64 words >= D), template ids ascending
-    std::vector<uint32_t> wrow((size_t)nbits + 1, 0);
-    uint32_t nrows = 0;
+    // the dense phase runs D rounded up to a multiple of 4 anyway (kernel template): use them all
+    const int D = std::min(w64, (pick_dense(sq, T, w64) + 3) / 4 * 4);
+    // one 32-byte postings row per narrow word (u64 words >= D), indexed by word id: a SHORT word
+    // (<= 16 templates) lists its template ids ascending, 0xFFFF padding; a LONG word stores its
+    // offset into the flat `plong` id list in entries 0-1, its length in entry 2, 0xFFFE in 15
+    std::vector<uint16_t> prow((size_t)nbits * kRowW, kNoTpl);
+    std::vector<uint32_t> loff((size_t)nbits, 0);
+    uint32_t nlong = 0;
     for (int64_t w = 0; w < nbits; ++w) {
-        wrow[(size_t)w] = nrows;
-        if (w / 64 >= D) nrows += (uint32_t)((plen[(size_t)w] + kRowW - 1) / kRowW);
+        loff[(size_t)w] = nlong;
+        if (w / 64 >= D && plen[(size_t)w] > kRowW) {
+            nlong += (uint32_t)plen[(size_t)w];
+            uint16_t* r = &prow[(size_t)w * kRowW];
+            r[0] = (uint16_t)(loff[(size_t)w] & 0xFFFF);
+            r[1] = (uint16_t)(loff[(size_t)w] >> 16);
+            r[2] = (uint16_t)plen[(size_t)w];
+            r[kRowW - 1] = kMore;
+        }
     }
-    wrow[(size_t)nbits] = nrows;
-    std::vector<uint16_t> prow((size_t)std::max<uint32_t>(nrows, 1) * kRowW, kNoTpl);
+    std::vector<uint16_t> plong((size_t)std::max<uint32_t>(nlong, 1), kNoTpl);
     std::vector<uint32_t> fill((size_t)nbits, 0);
     for (int32_t i = 0; i < T; ++i) {
         const uint64_t* r = t->lf_bits + (size_t)i * w64;
         for (int32_t p = D; p < w64; ++p)
             for (uint64_t x = r[p]; x; x &= x - 1) {
                 const int64_t w = (int64_t)p * 64 + __builtin_ctzll(x);
-                prow[(size_t)wrow[(size_t)w] * kRowW + fill[(size_t)w]++] = (uint16_t)i;
+                const uint32_t j = fill[(size_t)w]++;
+                if (plen[(size_t)w] <= kRowW) prow[(size_t)w * kRowW + j] = (uint16_t)i;
+                else plong[(size_t)loff[(size_t)w] + j] = (uint16_t)i;
             }
     }
     // dense prefix masks, template-major [T][kPostMaxDense]; template constants
@@ -276,30 +521,72 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
         tcv[i] = make_int4((int32_t)t->lf_size[i] - (int32_t)t->fields_set_size[i], t->length_slack[i],
                            t->length[i], t->is_cc[i] ? 1 : 0);
     int rc;
-    if ((rc = dalloc_bytes(&c->d_pwrow, wrow.size() * 4)) || (rc = dalloc_bytes(&c->d_prow, prow.size() * 2)) ||
+    if ((rc = dalloc_bytes(&c->d_prow, prow.size() * 2)) || (rc = dalloc_bytes(&c->d_povf, plong.size() * 2)) ||
         (rc = dalloc_bytes(&c->d_pdm, dm.size() * 8)) || (rc = dalloc_bytes(&c->d_ptc, tcv.size() * sizeof(int4))))
         return rc;
-    if (hipMemcpy(c->d_pwrow, wrow.data(), wrow.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(c->d_povf, plong.data(), plong.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_prow, prow.data(), prow.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_pdm, dm.data(), dm.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_ptc, tcv.data(), tcv.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "postings plan upload failed");
     c->post_dense = D;
+    const char* dg = getenv("DICE_POST_DIAG");
+    c->post_diag = dg && *dg ? atoi(dg) : 0;
     c->post_tpad = tpad;
-    c->post_rows = nrows;
+    // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
+    // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
+    c->post_fast = true;
+    for (int32_t i = 0; i < T; ++i) {
+        const int64_t base = (int64_t)t->lf_size[i] - (int64_t)t->fields_set_size[i];
+        if (!(t->lf_size[i] < (1u << 11) && base >= 1 && base < (1 << 18) && t->length[i] >= 0 &&
+              t->length[i] < (1 << 20) && 200 * (int64_t)t->lf_size[i] < 1024 * base))
+            c->post_fast = false;
+    }
+    c->post_tp = (T + 7) / 8 * 8;
+    c->post_rows = nlong;
     c->kind = 3;
     return DICE_OK;
 }
 
+template <int DP>
+static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s) {
+    const int64_t groups = (b->n + kPostFiles - 1) / kPostFiles;
+    auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
+                       (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
+                       (const uint64_t*)c->d_pdm, (uint16_t*)b->d_pdense);
+}
+
 template <bool kMatrix, int KM>
 static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t s) {
+    const size_t need = (size_t)b->capacity * c->post_tp * 2;
+    if (b->pdense_bytes < need) {
+        if (b->d_pdense) (void)hipFree(b->d_pdense);
+        b->d_pdense = nullptr;
+        b->pdense_bytes = 0;
+        int rc = dalloc_bytes(&b->d_pdense, need);
+        if (rc) return rc;
+        b->pdense_bytes = need;
+    }
+    if (c->post_dense == 0 || (c->post_diag & 1)) {
+        if (hipMemsetAsync(b->d_pdense, 0, (size_t)b->n * c->post_tp * 2, s) != hipSuccess)
+            return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
+    } else {
+        switch ((c->post_dense + 3) / 4) {
+            case 1: launch_dense<4>(c, b, s); break;
+            case 2: launch_dense<8>(c, b, s); break;
+            case 3: launch_dense<12>(c, b, s); break;
+            default: launch_dense<16>(c, b, s); break;
+        }
+    }
     const int64_t groups = (b->n + kPostFiles - 1) / kPostFiles;
-    hipLaunchKernelGGL((dice_post_kernel<kMatrix, KM>), dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
-                       (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tpad,
-                       (const uint64_t*)c->d_pdm, (const uint32_t*)c->d_pwrow, (const uint16_t*)c->d_prow,
+    auto kern = kMatrix ? dice_post_narrow_matrix<KM> : dice_post_narrow_match;
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
+                       (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
+                       (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const int4*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
-                       b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks);
-    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post_kernel launch failed");
+                       b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_diag, c->post_fast);
+    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post kernels launch failed");
 }
 
 int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
@@ -307,7 +594,8 @@ int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
 }
 
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s) {
-    return k <= 4 ? launch<true, 4>(c, b, 0.0, k, s) : launch<true, kTopKMax>(c, b, 0.0, k, s);
+    // a lane holds at most kPostMaxTpad / 64 templates: that many top-k slots serve any k <= 16
+    return k <= 4 ? launch<true, 4>(c, b, 0.0, k, s) : launch<true, kPostMaxTpad / kWave>(c, b, 0.0, k, s);
 }
 
 }  // namespace dice
