@@ -42,11 +42,11 @@ constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
 constexpr int kPostMaxDense = 16;        // dense prefix u64 words
 constexpr int kRowW = 16;                // template ids per postings row
-constexpr int kWordCap = 256;            // per-wave queue of narrow word ids
+constexpr int kWordCap = 192;            // per-wave queue of narrow word ids
 constexpr int kMidCap = 128;             // per-wave queue of words with 9-16 postings
 constexpr uint16_t kNoTpl = 0xFFFF;      // empty row entry
 constexpr uint16_t kMore = 0xFFFE;       // row entry 15: a long word (entries 0-1 offset, 2 length)
-constexpr int kLongCap = 128;            // per-wave queue of long words (offset, length)
+constexpr int kLongCap = 64;             // per-wave queue of long words (offset, length)
 constexpr int kChunks = 3;               // 64-word chunks of a file loaded together
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -96,8 +96,9 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
 }
 
-__device__ __forceinline__ void count(uint32_t* crow32, uint32_t id) {
-    atomicAdd(&crow32[id >> 1], 1u << ((id & 1) * 16));
+// Postings entries are byte offsets (4 * template) into the wave's u32 counter row.
+__device__ __forceinline__ void count(uint32_t* crow32, uint32_t off) {
+    atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(crow32) + off), 1u);
 }
 
 // Long words (> 16 narrow postings): 64 lanes per word, 4 words' id loads in flight.
@@ -254,26 +255,24 @@ template <bool kMatrix, int KM>
 __device__ __forceinline__ void post_narrow_body(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
     // diag (DICE_POST_DIAG, diagnostics only -- results are wrong): 2 skips the postings walk,
     // 4 skips the narrow-word extraction, 8 skips scoring
-    constexpr int kRowMax = kPostMaxTpad + 2;
     constexpr int kTJ = kPostMaxTpad / kWave;                  // templates per lane
-    __shared__ uint32_t cnt32[kPostWaves * kRowMax / 2];       // u16 counters, one row per wave
-    __shared__ int4 tcs[kPostMaxTpad];
+    __shared__ uint32_t cnt32[kPostWaves * kPostMaxTpad];      // u32 counters, one row per wave
+    __shared__ uint2 tcs[kPostMaxTpad];                        // packed template constants
     __shared__ uint32_t wq[kPostWaves][kWordCap];              // queued narrow word ids
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
     __shared__ uint32_t mq[kPostWaves][kMidCap];               // queued mid words
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
-    uint32_t* crow32 = cnt32 + wave * (kRowMax / 2);
-    uint16_t* crow = reinterpret_cast<uint16_t*>(crow32);
+    uint32_t* crow32 = cnt32 + wave * kPostMaxTpad;
     for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
-    for (int i = lane; i < kRowMax / 2; i += kWave) crow32[i] = 0;
+    for (int i = lane; i < kPostMaxTpad; i += kWave) crow32[i] = 0;
     __syncthreads();
 
     const int32_t pb0 = (diag & 4) ? w64 : D;
@@ -281,14 +280,17 @@ __device__ __forceinline__ void post_narrow_body(
         const int64_t file = f0 + fi;
         if (file >= n) break;   // wave-uniform
         const uint64_t* row = rows + file * w64;
-        // this file's dense partials start its counter row (a plain copy of u16 pairs: the row is
-        // zero here and this wave's postings adds come after it; no registers held across the walk)
+        // this file's dense partials start its counter row (a plain copy, u16 pairs widened: the
+        // row is zero here and this wave's postings adds come after it)
         {
             const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + file * tp);
 #pragma unroll
             for (int j = 0; j < (kPostMaxTpad / 2 + kWave - 1) / kWave; ++j) {
                 const int32_t i = lane + j * kWave;
-                if (i < tp / 2) crow32[i] = src[i];
+                if (i < tp / 2) {
+                    const uint32_t v = src[i];
+                    *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(v & 0xFFFFu, v >> 16);
+                }
             }
         }
         const uint32_t wf = wfp[file];
@@ -351,7 +353,7 @@ __device__ __forceinline__ void post_narrow_body(
         if (diag & 8) {
 #pragma unroll
             for (int j = 0; j < kTJ; ++j)
-                if (lane + j * kWave < T) crow[lane + j * kWave] = 0;
+                if (lane + j * kWave < T) crow32[lane + j * kWave] = 0;
             continue;
         }
         int32_t bi = -1, bd = 1;
@@ -364,9 +366,11 @@ __device__ __forceinline__ void post_narrow_body(
         for (int j = 0; j < kTJ; ++j) {
             const int32_t t = lane + j * kWave;
             if (t < T) {
-                const uint32_t ov = crow[t];
-                crow[t] = 0;
-                const int4 c = tcs[t];
+                const uint32_t ov = crow32[t];
+                crow32[t] = 0;
+                const uint2 pc = tcs[t];   // {len | cc << 31, base | slack << 16}
+                const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
+                                         (int32_t)(pc.x >> 31));
                 const int32_t den = dice_den(c, wf, lf);
                 if (kMatrix) {
                     mov[file * T + t] = ov;
@@ -418,7 +422,7 @@ __device__ __forceinline__ void post_narrow_body(
 __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_narrow_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
@@ -430,7 +434,7 @@ template <int KM>
 __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-    const int4* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
@@ -464,8 +468,13 @@ static int pick_dense(const std::vector<int64_t>& sq_per_u64, int32_t T, int32_t
 bool post_feasible(const dice_templates* t) {
     const int32_t tpad = (t->n_templates + 63) / 64 * 64;
     if (tpad > kPostMaxTpad) return false;
-    for (int32_t i = 0; i < t->n_templates; ++i)
-        if (t->lf_size[i] >= 65535u) return false;   // u16 counters
+    for (int32_t i = 0; i < t->n_templates; ++i) {
+        // u16 dense partials, packed constants: base in 16 bits, slack in int16, length in 31 bits
+        const int64_t base = (int64_t)t->lf_size[i] - (int64_t)t->fields_set_size[i];
+        if (t->lf_size[i] >= 65535u || base < 0 || base > 65535 || t->length_slack[i] < -32768 ||
+            t->length_slack[i] > 32767 || t->length[i] < 0)
+            return false;
+    }
     return true;
 }
 
@@ -508,26 +517,30 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
             for (uint64_t x = r[p]; x; x &= x - 1) {
                 const int64_t w = (int64_t)p * 64 + __builtin_ctzll(x);
                 const uint32_t j = fill[(size_t)w]++;
-                if (plen[(size_t)w] <= kRowW) prow[(size_t)w * kRowW + j] = (uint16_t)i;
-                else plong[(size_t)loff[(size_t)w] + j] = (uint16_t)i;
+                if (plen[(size_t)w] <= kRowW) prow[(size_t)w * kRowW + j] = (uint16_t)(4 * i);
+                else plong[(size_t)loff[(size_t)w] + j] = (uint16_t)(4 * i);
             }
     }
     // dense prefix masks, template-major [T][kPostMaxDense]; template constants
     std::vector<uint64_t> dm((size_t)T * kPostMaxDense, 0);
     for (int32_t i = 0; i < T; ++i)
         for (int d = 0; d < D; ++d) dm[(size_t)i * kPostMaxDense + d] = t->lf_bits[(size_t)i * w64 + d];
-    std::vector<int4> tcv((size_t)T);
-    for (int32_t i = 0; i < T; ++i)
-        tcv[i] = make_int4((int32_t)t->lf_size[i] - (int32_t)t->fields_set_size[i], t->length_slack[i],
-                           t->length[i], t->is_cc[i] ? 1 : 0);
+    // template constants packed for LDS: {length | cc << 31, base | slack << 16} (post_feasible
+    // checks the ranges)
+    std::vector<uint2> tcv((size_t)T);
+    for (int32_t i = 0; i < T; ++i) {
+        const uint32_t base = t->lf_size[i] - t->fields_set_size[i];
+        tcv[i] = make_uint2((uint32_t)t->length[i] | (t->is_cc[i] ? 0x80000000u : 0u),
+                            (base & 0xFFFFu) | ((uint32_t)(t->length_slack[i] & 0xFFFF) << 16));
+    }
     int rc;
     if ((rc = dalloc_bytes(&c->d_prow, prow.size() * 2)) || (rc = dalloc_bytes(&c->d_povf, plong.size() * 2)) ||
-        (rc = dalloc_bytes(&c->d_pdm, dm.size() * 8)) || (rc = dalloc_bytes(&c->d_ptc, tcv.size() * sizeof(int4))))
+        (rc = dalloc_bytes(&c->d_pdm, dm.size() * 8)) || (rc = dalloc_bytes(&c->d_ptc, tcv.size() * sizeof(uint2))))
         return rc;
     if (hipMemcpy(c->d_povf, plong.data(), plong.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_prow, prow.data(), prow.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_pdm, dm.data(), dm.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_ptc, tcv.data(), tcv.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(c->d_ptc, tcv.data(), tcv.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "postings plan upload failed");
     c->post_dense = D;
     const char* dg = getenv("DICE_POST_DIAG");
@@ -584,7 +597,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
-                       (const int4*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
+                       (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
                        b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_diag, c->post_fast);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post kernels launch failed");
 }
