@@ -12,7 +12,9 @@
 // reported as status 1 and normalized by the Python path instead, as are texts whose match
 // would nest deeper than the regex engine's frame limit (rx::TooDeep; e.g. thousands of
 // consecutive copyright lines under the copyright pattern's repeated group).
+#include <immintrin.h>
 #include <malloc.h>
+#include <cstdio>
 #include <pthread.h>
 #include <stdint.h>
 #include <string.h>
@@ -28,13 +30,70 @@
 #include <vector>
 
 #include "rx.h"
+#include "scan.h"
 
 using rx::Regex;
 using rx::Str;
 
+// Per-pass timing (diagnostic builds only: -DLH_PASS_TIMING, tools/host_prep_passes.py). PASS
+// wraps one step of the pipeline and adds its wall time to a per-thread table.
+#ifdef LH_PASS_TIMING
+#include <chrono>
+#include <mutex>
+namespace {
+struct PassTable {
+    std::vector<std::pair<const char*, double>> t;
+    void add(const char* name, double s) {
+        for (auto& e : t)
+            if (e.first == name) { e.second += s; return; }
+        t.emplace_back(name, s);
+    }
+};
+std::mutex g_pass_mu;
+PassTable g_pass_total;
+thread_local PassTable tl_pass;
+inline double pass_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void pass_flush() {
+    std::lock_guard<std::mutex> g(g_pass_mu);
+    for (auto& e : tl_pass.t) g_pass_total.add(e.first, e.second);
+    tl_pass.t.clear();
+}
+}  // namespace
+#define PASS(name, ...)                      \
+    do {                                     \
+        const double t0_ = pass_now();       \
+        __VA_ARGS__;                         \
+        tl_pass.add(name, pass_now() - t0_); \
+    } while (0)
+#else
+#define PASS(name, ...) \
+    do {                \
+        __VA_ARGS__;    \
+    } while (0)
+#endif
+
 namespace {
 
 const char32_t kSpace = U' ';
+
+// ASCII \w ([A-Za-z0-9_]) as a table
+constexpr struct AsciiWord {
+    uint8_t t[128];
+    constexpr AsciiWord() : t() {
+        for (int c = 0; c < 128; ++c)
+            t[c] = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+    }
+    constexpr uint8_t operator[](char32_t c) const { return t[c]; }
+} kAsciiWord;
+
+constexpr int kSpellSyms = 40;   // alphabet of the spelling keys + 1 (a-z, ' ', '-' in practice)
+
+// spelling prefilter slot of a \w run: its first and last characters and its length (15 bits)
+inline uint32_t spell_tok_slot(char32_t first, char32_t last, size_t len) {
+    return (first & 31u) | (last & 31u) << 5 | (uint32_t)std::min<size_t>(len, 31) << 10;
+}
 
 bool is_strip_char(char32_t c) { return c == 0 || c == ' ' || (c >= '\t' && c <= '\r'); }
 
@@ -45,10 +104,38 @@ Str ruby_strip(const Str& s) {
     return s.substr(a, b - a);
 }
 
-bool contains(const Str& s, const char* lit) {
-    Str l = rx::from_utf8(lit);
-    return s.find(l) != Str::npos;
+// Literal search over code points: a vector scan for positions holding the literal's first
+// and last characters, then a compare at each candidate (std::u32string::find steps one
+// character at a time).
+size_t find_lit(const Str& s, const char32_t* lit, size_t from = 0) {
+    size_t m = 0;
+    while (lit[m]) ++m;
+    const size_t n = s.size();
+    if (m == 0) return from <= n ? from : Str::npos;
+    if (n < m) return Str::npos;
+    const char32_t* p = s.data();
+    const char32_t c0 = lit[0], c1 = lit[m - 1];
+    const size_t last = n - m;   // last candidate start
+    size_t i = from;
+#if defined(__AVX2__)
+    const __m256i v0 = _mm256_set1_epi32((int)c0), v1 = _mm256_set1_epi32((int)c1);
+    for (; i + 8 <= last + 1; i += 8) {
+        const __m256i a = _mm256_cmpeq_epi32(_mm256_loadu_si256((const __m256i*)(p + i)), v0);
+        const __m256i b = _mm256_cmpeq_epi32(_mm256_loadu_si256((const __m256i*)(p + i + m - 1)), v1);
+        uint32_t mask = (uint32_t)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_and_si256(a, b)));
+        while (mask) {
+            const size_t j = i + (size_t)__builtin_ctz(mask);
+            if (std::char_traits<char32_t>::compare(p + j, lit, m) == 0) return j;
+            mask &= mask - 1;
+        }
+    }
+#endif
+    for (; i <= last; ++i)
+        if (p[i] == c0 && std::char_traits<char32_t>::compare(p + i, lit, m) == 0) return i;
+    return Str::npos;
 }
+
+bool contains(const Str& s, const char32_t* lit) { return find_lit(s, lit) != Str::npos; }
 
 // non-ASCII code points whose Python semantics match the ASCII rules used here: no case
 // mapping, not \w (str.isalnum() is False) -- punctuation, symbols, spaces, BOM.
@@ -70,20 +157,193 @@ bool safe_nonascii(char32_t c) {
 // to two characters) and U+03A3 Σ (str.lower() applies the Final_Sigma context rule).
 bool python_only(char32_t c) { return c == 0x130 || c == 0x131 || c == 0x17F || c == 0x212A || c == 0x3A3; }
 
+// Word keys for the wordset scan (content_helper.rb:109). Tokens are ASCII ([\w/-] with ASCII
+// \w, and apostrophes), so a token's first 16 characters pack into two 64-bit words (one byte
+// each); equal (lo, hi, len) is equality for tokens of <= 16 characters, longer ones also
+// compare their tails. The hash mixes the packed words (and an FNV-1a of a long token's tail).
+struct WordKey {
+    uint64_t lo = 0, hi = 0, h = 0;
+    uint32_t len = 0;
+};
+
+constexpr struct ByteMasks {
+    uint64_t lo[17], hi[17];   // [min(len, 16)]: the packed bytes that belong to the token
+    constexpr ByteMasks() : lo(), hi() {
+        for (int l = 0; l <= 16; ++l) {
+            lo[l] = l >= 8 ? ~0ull : (1ull << (8 * l)) - 1;
+            hi[l] = l >= 16 ? ~0ull : l <= 8 ? 0 : (1ull << (8 * (l - 8))) - 1;
+        }
+    }
+} kByteMasks;
+
+inline uint64_t key_mix(uint64_t lo, uint64_t hi, uint64_t len, uint64_t tail) {
+    uint64_t h = (lo ^ (hi * 0xC2B2AE3D27D4EB4FULL) ^ (len << 56) ^ tail) * 0x9E3779B97F4A7C15ULL;
+    return h ^ (h >> 29);
+}
+
+template <class C>
+inline uint64_t tail_hash(const C* p, size_t n) {   // FNV-1a over characters 16.. (long tokens)
+    uint64_t h = 1469598103934665603ULL;
+    for (size_t i = 16; i < n; ++i) {
+        h ^= (uint64_t)(uint32_t)p[i];
+        h *= 1099511628211ULL;
+    }
+    return h;
+}
+
+// key of p[0, n); `room` = characters readable from p (>= n): with >= 16 the packing reads a
+// full 16-character window and masks it
+inline WordKey word_key(const char32_t* p, size_t n, size_t room) {
+    WordKey k;
+    k.len = (uint32_t)n;
+    const size_t m = n < 16 ? n : 16;
+#if defined(__AVX2__)
+    if (room >= 16) {
+        const __m256i x = _mm256_packus_epi32(_mm256_loadu_si256((const __m256i*)p), _mm256_loadu_si256((const __m256i*)(p + 8)));
+        const __m256i y = _mm256_permute4x64_epi64(x, 0xD8);
+        const __m128i z = _mm_packus_epi16(_mm256_castsi256_si128(y), _mm256_extracti128_si256(y, 1));
+        k.lo = (uint64_t)_mm_cvtsi128_si64(z) & kByteMasks.lo[m];
+        k.hi = (uint64_t)_mm_extract_epi64(z, 1) & kByteMasks.hi[m];
+    } else
+#endif
+    {
+        (void)room;
+        for (size_t i = 0; i < m; ++i) {
+            const uint64_t b = (uint64_t)(p[i] < 255 ? p[i] : 255);
+            if (i < 8) k.lo |= b << (8 * i);
+            else k.hi |= b << (8 * (i - 8));
+        }
+    }
+    k.h = key_mix(k.lo, k.hi, n, n > 16 ? tail_hash(p, n) : 0);
+    return k;
+}
+
+inline WordKey word_key(const std::string& w) {
+    WordKey k;
+    const size_t n = w.size(), m = n < 16 ? n : 16;
+    k.len = (uint32_t)n;
+    for (size_t i = 0; i < m; ++i) {
+        const uint64_t b = (unsigned char)w[i];
+        if (i < 8) k.lo |= b << (8 * i);
+        else k.hi |= b << (8 * (i - 8));
+    }
+    k.h = key_mix(k.lo, k.hi, n, n > 16 ? tail_hash(w.data(), n) : 0);
+    return k;
+}
+
+inline bool tail_equal(const std::string& w, const char32_t* p) {
+    for (size_t i = 16; i < w.size(); ++i)
+        if ((char32_t)(unsigned char)w[i] != p[i]) return false;
+    return true;
+}
+
+// The template vocabulary: open addressing over packed word keys, words kept for the tail
+// compare of long words.
+struct VocabTable {
+    struct Slot {
+        uint64_t lo, hi;
+        uint32_t len;
+        int32_t id;   // -1: empty
+    };
+    std::vector<Slot> slot;
+    std::vector<std::string> words;
+    uint64_t mask = 0;
+    void build(int32_t n, const char* const* vocab) {
+        size_t cap = 16;
+        while (cap < 2 * (size_t)n + 1) cap <<= 1;
+        slot.assign(cap, Slot{0, 0, 0, -1});
+        mask = cap - 1;
+        words.assign(vocab, vocab + n);
+        for (int32_t i = 0; i < n; ++i) {
+            const WordKey k = word_key(words[i]);
+            size_t j = k.h & mask;
+            while (slot[j].id >= 0) j = (j + 1) & mask;
+            slot[j] = Slot{k.lo, k.hi, k.len, i};
+        }
+    }
+    int32_t find(const WordKey& k, const char32_t* p) const {
+        if (slot.empty()) return -1;
+        for (size_t j = k.h & mask;; j = (j + 1) & mask) {
+            const Slot& s = slot[j];
+            if (s.id < 0) return -1;
+            if (s.lo == k.lo && s.hi == k.hi && s.len == k.len && (k.len <= 16 || tail_equal(words[(size_t)s.id], p)))
+                return s.id;
+        }
+    }
+};
+
+// A file's distinct non-vocabulary words: open addressing over packed keys (start, len into
+// the text for the tail compare), reused by a thread across files (an epoch stamp marks the
+// live slots, so nothing is cleared per file).
+struct WordSet {
+    struct Slot {
+        uint64_t lo, hi;
+        uint32_t start, len, epoch;
+    };
+    std::vector<Slot> slot;
+    uint32_t cur = 0;
+    size_t count = 0, mask = 0;
+    const Str* text = nullptr;
+    void reset(const Str& s) {
+        size_t need = 16;
+        while (need < s.size() + 32) need <<= 1;   // distinct words <= chars / 2 + 1: load <= 1/2
+        if (need > slot.size()) {
+            slot.assign(need, Slot{0, 0, 0, 0, 0});
+            cur = 0;
+        }
+        mask = slot.size() - 1;
+        if (++cur == 0) {   // epoch wrapped: clear once
+            for (auto& e : slot) e.epoch = 0;
+            cur = 1;
+        }
+        count = 0;
+        text = &s;
+    }
+    // true when the token [a, a + k.len) is a new word
+    bool insert(size_t a, const WordKey& k) {
+        for (size_t j = k.h & mask;; j = (j + 1) & mask) {
+            Slot& s = slot[j];
+            if (s.epoch != cur) {
+                s = Slot{k.lo, k.hi, (uint32_t)a, k.len, cur};
+                ++count;
+                return true;
+            }
+            if (s.lo == k.lo && s.hi == k.hi && s.len == k.len &&
+                (k.len <= 16 || text->compare(s.start, k.len, *text, a, k.len) == 0))
+                return false;
+        }
+    }
+    bool contains(const std::string& w) const {
+        const WordKey k = word_key(w);
+        for (size_t j = k.h & mask;; j = (j + 1) & mask) {
+            const Slot& s = slot[j];
+            if (s.epoch != cur) return false;
+            if (s.lo == k.lo && s.hi == k.hi && s.len == k.len && (k.len <= 16 || tail_equal(w, text->data() + s.start)))
+                return true;
+        }
+    }
+};
+
 struct Ctx {
     std::map<std::string, Regex> re;
     std::vector<std::pair<Str, Str>> spell;
-    std::vector<int> spell_first2[128 * 128];   // spell indices by first two characters, union order kept
+    // spelling keys as a trie over a small alphabet (spell_sym: ASCII -> 1..kSpellSyms-1, 0 = not
+    // in any key); node 0 is the root, child 0 = none; spell_key: key index ending at a node
+    uint8_t spell_sym[128] = {};
+    std::vector<int32_t> spell_trie;
+    std::vector<int32_t> spell_key;
+    uint64_t spell_tok[(1u << 15) / 64] = {};   // spell_tok_slot of every key's first \w run
     // Unicode tables (lh_set_unicode): Python str.lower() of non-ASCII code points
     bool unicode = false;
     std::unordered_map<char32_t, char32_t> lower;
-    std::unordered_map<std::string, int32_t> vocab;
+    VocabTable vocab;
     int32_t n_vocab = 0, w64 = 0;
     // templates (Exact)
     int32_t n_templates = 0;
     std::vector<uint64_t> lf_bits;                  // [T][w64]
     std::vector<uint32_t> full_size;                // |wordset|
     std::vector<std::vector<std::string>> fields;   // field words in the wordset
+    std::vector<std::vector<int32_t>> field_ids;    // their vocabulary ids, or -1
     std::string err;
 
     const Regex& R(const char* name) const { return re.at(name); }
@@ -96,12 +356,13 @@ struct Normalizer {
 
     // squeeze(' ').strip in place (String#squeeze / #strip: only ' ' runs, \0\t\n\v\f\r ends)
     void squeeze_strip() {
-        size_t w = 0;
-        for (size_t r = 0; r < cur.size(); ++r) {
-            if (cur[r] == kSpace && w > 0 && cur[w - 1] == kSpace) continue;
-            cur[w++] = cur[r];
-        }
-        cur.resize(w);
+        char32_t* p = cur.data();
+        const size_t n = cur.size();
+        const size_t r = scan::find_double_space(p, 0, n);   // nothing to squeeze before it
+        if (r < n) cur.resize(scan::squeeze_runs(p, r, r, n, true, false));
+        strip_ends();
+    }
+    void strip_ends() {
         size_t b = cur.size();
         while (b > 0 && is_strip_char(cur[b - 1])) --b;
         cur.resize(b);
@@ -161,132 +422,184 @@ struct Normalizer {
     // path has ASCII word characters only, so \b is the ASCII boundary.
     void spelling() {
         const size_t n = cur.size();
+        const char32_t* p = cur.data();
         auto word = [](char32_t ch) {   // Python \b's \w
-            return ch < 128 ? ((ch | 32) >= 'a' && (ch | 32) <= 'z') || (ch >= '0' && ch <= '9') || ch == '_'
-                            : rx::is_word_char(ch);
+            return ch < 128 ? kAsciiWord[ch] != 0 : rx::is_word_char(ch);
         };
-        // next hit at or after i: only word starts are candidates (every key starts with a
-        // letter, so \b(?:key) can only match there); skips whole words otherwise
-        auto next_hit = [&](size_t i, size_t& at, size_t& klen) -> const Str* {
-            while (i < n) {
-                const char32_t ch = cur[i];
-                if (!word(ch)) {
-                    ++i;
-                    continue;
+        // the key matching at word start i, or -1: the keys are walked in a trie and, of the
+        // keys ending at a \b, the first in union order wins (Regexp.union alternation order)
+        auto match_at = [&](size_t i, size_t& klen) -> int {
+            int node = 0, best = -1;
+            for (size_t j = i; j < n; ++j) {
+                const char32_t cj = p[j];
+                const int sym = cj < 128 ? c.spell_sym[cj] : 0;
+                if (!sym) break;
+                node = c.spell_trie[(size_t)node * kSpellSyms + sym];
+                if (node <= 0) break;
+                const int ki = c.spell_key[node];
+                if (ki >= 0 && (best < 0 || ki < best) && (j + 1 == n || !word(p[j + 1]))) {
+                    best = ki;
+                    klen = j + 1 - i;
                 }
-                if (ch < 128 && i + 1 < n && cur[i + 1] < 128)
-                    for (int si : c.spell_first2[ch * 128 + cur[i + 1]]) {
-                        const Str& k = c.spell[si].first;
-                        if (k.size() <= n - i && cur.compare(i, k.size(), k) == 0 &&
-                            (i + k.size() == n || !word(cur[i + k.size()]))) {
-                            at = i;
-                            klen = k.size();
-                            return &c.spell[si].second;
-                        }
-                    }
-                while (i < n && word(cur[i])) ++i;
             }
-            return nullptr;
+            return best;
         };
-        size_t at = 0, klen = 0;
-        const Str* rep = next_hit(0, at, klen);
-        if (!rep) return;   // no varietal word: nothing to rebuild
+        // Every key starts with a letter, so \b(?:key) matches only at a word start, and the
+        // \w run starting there equals the key's first \w run (keys end in a letter, and \b
+        // follows). Word starts come from 64-character \w masks; a start is tried only when
+        // its run's (first, last, length) is that of some key's first run (spell_tok).
         Str out;
-        out.reserve(n);
-        size_t i = 0;
-        while (rep) {
-            out.append(cur, i, at - i);
-            out += *rep;
-            i = at + klen;
-            rep = next_hit(i, at, klen);
+        size_t copied = 0;   // cur[0, copied) is in out (or there is no match yet)
+        uint64_t prev_word = 0;
+        for (size_t b0 = 0; b0 < n; b0 += 64) {
+            const size_t k = std::min<size_t>(64, n - b0);
+            uint64_t hi;
+            uint64_t w = scan::ascii_word_mask(p + b0, k, &hi);
+            while (hi) {
+                const int j = __builtin_ctzll(hi);
+                hi &= hi - 1;
+                if (rx::is_word_char(p[b0 + (size_t)j])) w |= 1ull << j;
+            }
+            uint64_t starts = w & ~((w << 1) | prev_word);
+            prev_word = w >> 63;
+            while (starts) {
+                const size_t off = (size_t)__builtin_ctzll(starts);
+                starts &= starts - 1;
+                const size_t s0 = b0 + off;
+                if (s0 < copied) continue;
+                const uint64_t rest = ~w >> off;   // bit 0 clear: p[s0] is a word character
+                size_t len;
+                if (rest) {
+                    len = (size_t)__builtin_ctzll(rest);
+                    if (s0 + len > n) len = n - s0;
+                } else {
+                    len = 64 - off;
+                    while (s0 + len < n && word(p[s0 + len])) ++len;
+                }
+                if (!spell_tok_hit(p[s0], p[s0 + len - 1], len)) continue;
+                size_t klen = 0;
+                const int key = match_at(s0, klen);
+                if (key < 0) continue;
+                if (out.empty() && copied == 0) out.reserve(n + 16);
+                out.append(cur, copied, s0 - copied);
+                out += c.spell[(size_t)key].second;
+                copied = s0 + klen;
+            }
         }
-        out.append(cur, i, Str::npos);
+        if (copied == 0 && out.empty()) return;   // no varietal word: nothing to rebuild
+        out.append(cur, copied, Str::npos);
         cur.swap(out);
         clean = false;
+    }
+    bool spell_tok_hit(char32_t first, char32_t last, size_t len) const {
+        const uint32_t h = spell_tok_slot(first, last, len);
+        return (c.spell_tok[h >> 6] >> (h & 63)) & 1;
     }
 
     // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip, in place
     void collapse_whitespace() {
-        size_t w = 0;
-        for (size_t r = 0; r < cur.size(); ++r) {
-            const char32_t ch = cur[r];
-            const bool ws = ch == ' ' || (ch >= '\t' && ch <= '\r');
-            if (ws) {
-                if (w == 0 || cur[w - 1] != ' ') cur[w++] = ' ';
-            } else {
-                cur[w++] = ch;
-            }
-        }
-        cur.resize(w);
-        // no ' ' runs are left, so squeeze(' ') is the identity: strip only
-        size_t b = cur.size();
-        while (b > 0 && is_strip_char(cur[b - 1])) --b;
-        cur.resize(b);
-        size_t a = 0;
-        while (a < cur.size() && is_strip_char(cur[a])) ++a;
-        if (a) cur.erase(0, a);
+        cur.resize(scan::squeeze_runs(cur.data(), 0, 0, cur.size(), false, true));
+        strip_ends();   // no ' ' runs are left, so squeeze(' ') is the identity: strip only
         clean = true;
     }
 
     // content_without_title_and_version + content_normalized (content_helper.rb:144-168)
     Str run(const Str& content) {
-        cur = ruby_strip(content);
-        strip_re(c.R("hrs"));
-        strip_comments();
-        strip_re(c.R("markdown_headings"));
+        PASS("strip", cur = ruby_strip(content));
+        PASS("hrs", strip_re(c.R("hrs")));
+        PASS("comments", strip_comments());
+        PASS("markdown_headings", strip_re(c.R("markdown_headings")));
         // \[(.+?)\]\(.+?\) needs a literal "](": without one the lazy scans from every '[' are wasted
-        if (contains(cur, "](")) sub_re(c.R("link_markup"), U"\\1");
-        strip_title();
-        strip_re(c.R("version"));
-        for (auto& ch : cur) {
-            if (ch < 128) {
-                if (ch >= 'A' && ch <= 'Z') ch += 32;
-            } else if (c.unicode) {
-                auto it = c.lower.find(ch);
-                if (it != c.lower.end()) ch = it->second;
+        PASS("link_markup", if (contains(cur, U"](")) sub_re(c.R("link_markup"), U"\\1"));
+        PASS("title", strip_title());
+        PASS("version", strip_re(c.R("version")));
+        // downcase, then (moved ahead of lists/https, with which they commute: neither pattern
+        // reads '&' or a quote character other than as lists' copied [^\n]) '&' -> 'and' and the
+        // quote characters -> "'" (content_helper.rb:34-41), one pass
+        PASS("downcase_amp_quote", {
+            size_t amps = 0;
+            for (auto& ch : cur) {
+                if (ch < 128) {
+                    if (ch >= 'A' && ch <= 'Z') ch += 32;
+                    else if (ch == '"' || ch == '`') ch = '\'';
+                    else if (ch == '&') ++amps;
+                } else if (ch == 0x2018 || ch == 0x2019 || ch == 0x201C || ch == 0x201D) {
+                    ch = '\'';
+                } else if (c.unicode) {
+                    auto it = c.lower.find(ch);
+                    if (it != c.lower.end()) ch = it->second;
+                }
             }
-        }
-        sub_re(c.R("lists"), U"- \\1");
-        sub_re(c.R("https"), U"https:");
-        {   // '&' -> 'and'
-            Str out;
-            for (char32_t ch : cur) {
-                if (ch == '&') out += U"and";
-                else out.push_back(ch);
+            if (amps) {
+                Str out;
+                out.reserve(cur.size() + 2 * amps);
+                for (char32_t ch : cur) {
+                    if (ch == '&') out += U"and";
+                    else out.push_back(ch);
+                }
+                cur.swap(out);
             }
-            cur.swap(out);
-        }
-        sub_re(c.R("dashes"), U"-");
-        sub_re(c.R("quote"), U"'");
-        if (has_hyphen_break(cur)) sub_re(c.R("hyphenated"), U"\\1-\\2");
-        spelling();
-        sub_re(c.R("span_markup"), U"\\1");
-        sub_re(c.R("bullet"), U"\n\n- ");
-        sub_re(c.R("bullet_paren"), U")(");
+            clean = false;
+        });
+        PASS("lists", sub_re(c.R("lists"), U"- \\1"));
+        // the literal 'http:' (content_helper.rb:35) without the regex engine
+        PASS("https", {
+            size_t at = find_lit(cur, U"http:");
+            if (at != Str::npos) {
+                Str out;
+                size_t i = 0;
+                for (; at != Str::npos; at = find_lit(cur, U"http:", i)) {
+                    out.append(cur, i, at - i);
+                    out += U"https:";
+                    i = at + 5;
+                }
+                out.append(cur, i, Str::npos);
+                cur.swap(out);
+                clean = false;
+            }
+        });
+        // (?<!^)([\u2014\u2013-]+)(?!$) -> '-' changes nothing unless a run holds an em/en dash or
+        // two hyphens: skip the regex when the text has neither
+        PASS("dashes", {
+            bool may = false;
+            for (size_t i = 0; i < cur.size() && !may; ++i)
+                may = cur[i] == 0x2014 || cur[i] == 0x2013 || (cur[i] == '-' && i + 1 < cur.size() && cur[i + 1] == '-');
+            if (may) sub_re(c.R("dashes"), U"-");
+        });
+        PASS("hyphenated", if (has_hyphen_break(cur)) sub_re(c.R("hyphenated"), U"\\1-\\2"));
+        PASS("spelling", spelling());
+        PASS("span_markup", sub_re(c.R("span_markup"), U"\\1"));
+        PASS("bullet", sub_re(c.R("bullet"), U"\n\n- "));
+        PASS("bullet_paren", sub_re(c.R("bullet_paren"), U")("));
         // STRIP_METHODS (content_helper.rb:89-105)
-        strip_re(c.R("bom"));
-        if (contains(cur, "creative commons")) { strip_re(c.R("cc_dedication")); strip_re(c.R("cc_wiki")); }
-        if (contains(cur, "associating cc0")) {
-            strip_re(c.R("cc_legal_code")); strip_re(c.R("cc0_info")); strip_re(c.R("cc0_disclaimer"));
-        }
-        if (contains(cur, "unlicense")) strip_re(c.R("unlicense_info"));
-        sub_re(c.R("border_markup"), U"\\1");
-        strip_title();
-        strip_re(c.R("version"));
-        strip_re(c.R("url"));
-        strip_copyright();
-        strip_title();
-        strip_re(c.R("block_markup"));
-        strip_re(c.R("developed_by"));
-        {
+        PASS("bom", strip_re(c.R("bom")));
+        PASS("cc_optional", if (contains(cur, U"creative commons")) {
+            strip_re(c.R("cc_dedication"));
+            strip_re(c.R("cc_wiki"));
+        });
+        PASS("cc0_optional", if (contains(cur, U"associating cc0")) {
+            strip_re(c.R("cc_legal_code"));
+            strip_re(c.R("cc0_info"));
+            strip_re(c.R("cc0_disclaimer"));
+        });
+        PASS("unlicense_optional", if (contains(cur, U"unlicense")) strip_re(c.R("unlicense_info")));
+        PASS("borders", sub_re(c.R("border_markup"), U"\\1"));
+        PASS("title2", strip_title());
+        PASS("version2", strip_re(c.R("version")));
+        PASS("url", strip_re(c.R("url")));
+        PASS("copyright", strip_copyright());
+        PASS("title3", strip_title());
+        PASS("block_markup", strip_re(c.R("block_markup")));
+        PASS("developed_by", strip_re(c.R("developed_by")));
+        PASS("end_of_terms", {
             std::vector<long> caps;
             if (c.R("end_of_terms").search(cur, 0, caps)) {
                 cur.resize((size_t)caps[0]);
                 clean = false;
             }
-        }
-        collapse_whitespace();
-        strip_re(c.R("mit_optional"));
+        });
+        PASS("whitespace", collapse_whitespace());
+        PASS("mit_optional", strip_re(c.R("mit_optional")));
         return cur;
     }
 };
@@ -296,21 +609,49 @@ inline bool wchar(char32_t c) {
     return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_' || c == '/' || c == '-';
 }
 
+// The regex's own loop from a token start: returns the token's end
+inline size_t word_end(const char32_t* s, size_t i, size_t n) {
+    while (i < n && wchar(s[i])) {
+        const char32_t ch = s[i++];
+        if (i < n && s[i] == '\'') {
+            if (i + 1 < n && s[i + 1] == 's') i += 2;
+            else if (ch == 's') i += 1;
+        }
+    }
+    return i;
+}
+
+// Tokens are the runs of [\w/-] (64-character masks), except that a run followed by '\'' is
+// re-scanned by the regex's loop ('s and s' continue a token; an apostrophe never starts one).
+// A token ends at a character outside [\w/-], so the next one starts at a run start.
 template <class F>
 void scan_words(const Str& s, F&& emit) {
-    size_t i = 0;
+    const char32_t* p = s.data();
     const size_t n = s.size();
-    while (i < n) {
-        if (!wchar(s[i])) { ++i; continue; }
-        const size_t a = i;
-        while (i < n && wchar(s[i])) {
-            const char32_t ch = s[i++];
-            if (i + 1 < n + 1 && i < n && s[i] == '\'') {
-                if (i + 1 < n && s[i + 1] == 's') i += 2;
-                else if (ch == 's') i += 1;
+    size_t resume = 0;   // end of the last token
+    uint64_t prev = 0;
+    for (size_t b0 = 0; b0 < n; b0 += 64) {
+        uint64_t hi;
+        const uint64_t w = scan::ascii_word_mask<true>(p + b0, std::min<size_t>(64, n - b0), &hi);
+        uint64_t starts = w & ~((w << 1) | prev);
+        prev = w >> 63;
+        while (starts) {
+            const size_t off = (size_t)__builtin_ctzll(starts);
+            starts &= starts - 1;
+            const size_t a = b0 + off;
+            if (a < resume) continue;
+            const uint64_t rest = ~w >> off;
+            size_t e;
+            if (rest) {
+                e = std::min(n, a + (size_t)__builtin_ctzll(rest));
+            } else {
+                e = b0 + 64;
+                while (e < n && wchar(p[e])) ++e;
             }
+            if (e < n && p[e] == '\'') e = word_end(p, a, n);
+            emit(a, e);
+            resume = e;
         }
-        emit(a, i);
     }
 }
 
@@ -336,6 +677,8 @@ struct FileOut {
 };
 
 void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o);
+
+thread_local WordSet tl_words;
 
 // prep_one with the regex engine's depth abort mapped to "use the Python path"
 void prep_one(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o) {
@@ -379,25 +722,28 @@ void run_workers(int32_t nthreads, F& work) {
 }
 
 void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o) {
-    Str content = rx::from_utf8(std::string(data, (size_t)len));
-    if (is_file) {   // universal newline (project_file.rb:41)
-        Str t;
-        t.reserve(content.size());
-        for (size_t i = 0; i < content.size(); ++i) {
+    Str content;
+    PASS("decode", content = rx::from_utf8(data, (size_t)len));
+    if (is_file) {   // universal newline (project_file.rb:41), in place
+        const size_t n = content.size();
+        size_t w = 0;
+        for (size_t i = 0; i < n; ++i) {
             if (content[i] == '\r') {
-                t.push_back('\n');
-                if (i + 1 < content.size() && content[i + 1] == '\n') ++i;
-            } else t.push_back(content[i]);
+                content[w++] = '\n';
+                if (i + 1 < n && content[i + 1] == '\n') ++i;
+            } else {
+                content[w++] = content[i];
+            }
         }
-        content.swap(t);
+        content.resize(w);
     }
     for (char32_t ch : content)
         if (ch >= 0x80 && (c.unicode ? python_only(ch) : !safe_nonascii(ch))) { o.status = 1; return; }
     if (extname_is_html(filename)) { o.status = 1; return; }
     std::vector<long> caps;
     const Str stripped = ruby_strip(content);
-    o.cc = c.R("cc_false_positive").search(stripped, 0, caps);
-    o.copyright = c.R("copyright_match").search(stripped, 0, caps);
+    PASS("cc_flag", o.cc = c.R("cc_false_positive").search(stripped, 0, caps));
+    PASS("copyright_matcher", o.copyright = c.R("copyright_match").search(stripped, 0, caps));
     Normalizer nz{c, Str()};
     o.normalized = nz.run(content);
 }
@@ -419,14 +765,38 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
     Ctx* c = new Ctx();
     try {
         for (int32_t i = 0; i < n_patterns; ++i) c->re.emplace(names[i], Regex(patterns[i], flags[i]));
+        int nsym = 1;
         for (int32_t i = 0; i < n_spell; ++i) {
             c->spell.push_back({rx::from_utf8(spell_from[i]), rx::from_utf8(spell_to[i])});
             const Str& k = c->spell.back().first;
-            if (k.size() < 2 || k[0] >= 128 || k[1] >= 128)
-                throw std::runtime_error("spelling keys: >= 2 characters, ASCII first two");
-            c->spell_first2[k[0] * 128 + k[1]].push_back(i);
+            if (k.empty() || k[0] >= 128 || !kAsciiWord[k[0]]) throw std::runtime_error("spelling keys: ASCII word start");
+            for (char32_t ch : k) {
+                if (ch >= 128) throw std::runtime_error("spelling keys: ASCII only");
+                if (!c->spell_sym[ch]) c->spell_sym[ch] = (uint8_t)nsym++;
+            }
         }
-        for (int32_t i = 0; i < n_vocab; ++i) c->vocab.emplace(vocab[i], i);
+        if (nsym > kSpellSyms) throw std::runtime_error("spelling keys: alphabet too large");
+        c->spell_trie.assign(kSpellSyms, 0);
+        c->spell_key.assign(1, -1);
+        for (int32_t i = 0; i < n_spell; ++i) {
+            int node = 0;
+            for (char32_t ch : c->spell[(size_t)i].first) {
+                int32_t& next = c->spell_trie[(size_t)node * kSpellSyms + c->spell_sym[ch]];
+                if (next == 0) {
+                    next = (int32_t)c->spell_key.size();
+                    c->spell_key.push_back(-1);
+                    c->spell_trie.resize(c->spell_trie.size() + kSpellSyms, 0);
+                }
+                node = c->spell_trie[(size_t)node * kSpellSyms + c->spell_sym[ch]];
+            }
+            if (c->spell_key[(size_t)node] < 0) c->spell_key[(size_t)node] = i;   // first in union order
+            const Str& k = c->spell[(size_t)i].first;
+            size_t len = 0;
+            while (len < k.size() && kAsciiWord[k[len]]) ++len;
+            const uint32_t h = spell_tok_slot(k[0], k[len - 1], len);
+            c->spell_tok[h >> 6] |= 1ull << (h & 63);
+        }
+        c->vocab.build(n_vocab, vocab);
         c->n_vocab = n_vocab;
         c->w64 = (n_vocab + 63) / 64;
         const char* need[] = {"hrs", "comment_markup", "markdown_headings", "link_markup", "title", "version",
@@ -456,8 +826,15 @@ int lh_set_templates(lh_ctx* ctx, int32_t n_templates, const uint64_t* lf_bits, 
     c->lf_bits.assign(lf_bits, lf_bits + (size_t)n_templates * c->w64);
     c->full_size.assign(wordset_size, wordset_size + n_templates);
     c->fields.assign(n_templates, {});
+    c->field_ids.assign(n_templates, {});
     for (int32_t t = 0; t < n_templates; ++t)
-        for (int32_t k = field_off[t]; k < field_off[t + 1]; ++k) c->fields[t].push_back(field_words[k]);
+        for (int32_t k = field_off[t]; k < field_off[t + 1]; ++k) {
+            c->fields[t].push_back(field_words[k]);
+            // a field word can still be vocabulary (another template's word): then its presence is
+            // the file's vocabulary bit, else the WordSet holds it
+            const Str w = rx::from_utf8(field_words[k], strlen(field_words[k]));
+            c->field_ids[t].push_back(c->vocab.find(word_key(w.data(), w.size(), w.size()), w.data()));
+        }
     return 0;
 }
 
@@ -512,36 +889,63 @@ int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t
                 status[f] = (uint8_t)o.status;
                 if (o.status) continue;
                 std::fill(row.begin(), row.end(), 0);
-                std::unordered_set<std::string> words;
-                std::string w;
-                scan_words(o.normalized, [&](size_t a, size_t b) {
-                    w.clear();
-                    for (size_t k = a; k < b; ++k) w.push_back((char)o.normalized[k]);   // ASCII only
-                    if (words.insert(w).second) {
-                        auto it = c->vocab.find(w);
-                        if (it != c->vocab.end()) row[(size_t)it->second >> 6] |= 1ULL << (it->second & 63);
+                // distinct words: vocabulary words are de-duplicated by their bit in `row`, the
+                // others through the per-thread WordSet
+                WordSet& words = tl_words;
+                words.reset(o.normalized);
+                size_t n_vocab_words = 0;
+                PASS("wordset", scan_words(o.normalized, [&](size_t a, size_t b) {
+                    const char32_t* p = o.normalized.data() + a;
+                    const WordKey k = word_key(p, b - a, o.normalized.size() - a);
+                    const int32_t id = c->vocab.find(k, p);
+                    if (id >= 0) {
+                        uint64_t& wd = row[(size_t)id >> 6];
+                        const uint64_t bit = 1ULL << (id & 63);
+                        n_vocab_words += (wd & bit) == 0;
+                        wd |= bit;
+                    } else {
+                        words.insert(a, k);
                     }
-                });
+                }));
+                const size_t n_words = n_vocab_words + words.count;
                 memcpy(bits + (size_t)f * c->w64, row.data(), sizeof(uint64_t) * (size_t)c->w64);
-                wf[f] = (uint32_t)words.size();
+                wf[f] = (uint32_t)n_words;
                 length[f] = (int32_t)o.normalized.size();
                 cc[f] = o.cc;
                 copyright[f] = o.copyright;
                 int32_t ex = -1;
-                for (int32_t t = 0; t < c->n_templates && ex < 0; ++t) {
-                    if (c->full_size[t] != words.size()) continue;
+                PASS("exact", for (int32_t t = 0; t < c->n_templates && ex < 0; ++t) {
+                    if (c->full_size[t] != n_words) continue;
                     const uint64_t* L = c->lf_bits.data() + (size_t)t * c->w64;
                     bool ok = true;
                     for (int32_t k = 0; k < c->w64 && ok; ++k) ok = (row[k] & L[k]) == L[k];
-                    for (size_t k = 0; k < c->fields[t].size() && ok; ++k) ok = words.count(c->fields[t][k]) > 0;
+                    for (size_t k = 0; k < c->fields[t].size() && ok; ++k) {
+                        const int32_t id = c->field_ids[t][k];
+                        ok = id >= 0 ? (row[(size_t)id >> 6] >> (id & 63) & 1) != 0 : words.contains(c->fields[t][k]);
+                    }
                     if (ok) ex = t;
-                }
+                });
                 exact[f] = ex;
             }
         }
+#ifdef LH_PASS_TIMING
+        pass_flush();
+#endif
     };
     run_workers(nthreads, work);
     return 0;
 }
+
+#ifdef LH_PASS_TIMING
+// Diagnostic builds: "name seconds\n" per pass, summed over every thread since the last call.
+int64_t lh_pass_timing(char* buf, int64_t cap) {
+    std::lock_guard<std::mutex> g(g_pass_mu);
+    std::string out;
+    for (auto& e : g_pass_total.t) out += std::string(e.first) + " " + std::to_string(e.second) + "\n";
+    g_pass_total.t.clear();
+    if (buf && cap > 0) snprintf(buf, (size_t)cap, "%s", out.c_str());
+    return (int64_t)out.size();
+}
+#endif
 
 }  // extern "C"

@@ -3,22 +3,45 @@
 // ordered alternation, greedy / lazy quantifiers with backtracking, fixed-width lookbehind.
 #include "rx.h"
 
+#include <algorithm>
 #include <stdexcept>
+
+#include "scan.h"
 
 namespace rx {
 
 // ---- UTF-8 ---------------------------------------------------------------------------
 // UTF-8 -> code points with Python's errors='ignore' semantics: an invalid sequence's
 // maximal valid prefix (at least one byte) is dropped (project_file.rb:38-40 replace: '').
-Str from_utf8(const std::string& s) {
+Str from_utf8(const std::string& s) { return from_utf8(s.data(), s.size()); }
+
+// UTF-8 -> code points; invalid sequences drop their maximal subpart (Ruby's
+// String#scrub('') as project_file.rb:39 applies it). ASCII runs are widened without checks.
+Str from_utf8(const char* data, size_t n) {
     Str out;
-    out.reserve(s.size());
-    const size_t n = s.size();
-    size_t i = 0;
-    auto byte = [&](size_t k) { return (unsigned)(unsigned char)s[k]; };
+    out.resize(n);   // code points <= bytes
+    char32_t* o = &out[0];
+    size_t w = 0, i = 0;
+    auto byte = [&](size_t k) { return (unsigned)(unsigned char)data[k]; };
     while (i < n) {
         const unsigned c = byte(i);
-        if (c < 0x80) { out.push_back(c); ++i; continue; }
+        if (c < 0x80) {
+#if defined(__AVX2__)
+            if (i + 16 <= n) {   // 16 ASCII bytes at once (w <= i, so w + 16 <= n)
+                const __m128i b = _mm_loadu_si128((const __m128i*)(data + i));
+                if (_mm_movemask_epi8(b) == 0) {
+                    _mm256_storeu_si256((__m256i*)(o + w), _mm256_cvtepu8_epi32(b));
+                    _mm256_storeu_si256((__m256i*)(o + w + 8), _mm256_cvtepu8_epi32(_mm_srli_si128(b, 8)));
+                    w += 16;
+                    i += 16;
+                    continue;
+                }
+            }
+#endif
+            o[w++] = c;
+            ++i;
+            continue;
+        }
         int need;
         unsigned lo = 0x80, hi = 0xBF;   // allowed range of the first continuation byte
         char32_t cp;
@@ -34,15 +57,16 @@ Str from_utf8(const std::string& s) {
         bool ok = true;
         for (; k <= (size_t)need; ++k) {
             if (i + k >= n) { ok = false; break; }
-            const unsigned b = byte(i + k);
+            const unsigned bb = byte(i + k);
             const unsigned l = k == 1 ? lo : 0x80, h = k == 1 ? hi : 0xBF;
-            if (b < l || b > h) { ok = false; break; }
-            cp = (cp << 6) | (b & 0x3F);
+            if (bb < l || bb > h) { ok = false; break; }
+            cp = (cp << 6) | (bb & 0x3F);
         }
         if (!ok) { i += k; continue; }   // drop the maximal subpart
-        out.push_back(cp);
-        i += need + 1;
+        o[w++] = cp;
+        i += (size_t)need + 1;
     }
+    out.resize(w);
     return out;
 }
 
@@ -495,6 +519,58 @@ static void first_chars(const NodeP& n, std::vector<bool>& set, bool& nonascii, 
     }
 }
 
+// The exact set of code points a match of n can start with, when it has at most kMaxFirst
+// members (false otherwise, or when n can match empty: nullable).
+static constexpr size_t kMaxFirst = 8;
+static bool first_list(const NodeP& n, std::vector<char32_t>& out, bool& nullable) {
+    auto add = [&](char32_t c, bool icase) {
+        out.push_back(c);
+        if (icase && c < 128) {   // fold() is ASCII-only: a letter matches its two cases
+            out.push_back(fold(c));
+            if (c >= 'a' && c <= 'z') out.push_back(c - 32);
+        }
+    };
+    switch (n->kind) {
+        case Node::LIT: add(n->ch, n->icase); nullable = false; break;
+        case Node::ANY: return false;
+        case Node::CLASS:
+            if (n->negate) return false;
+            for (auto& r : n->ranges) {
+                if (r.second - r.first >= kMaxFirst) return false;
+                for (char32_t c = r.first; c <= r.second; ++c) add(c, n->icase);
+            }
+            nullable = false;
+            break;
+        case Node::SEQ:
+            nullable = true;
+            for (auto& k : n->kids) {
+                bool nl = false;
+                if (!first_list(k, out, nl)) return false;
+                if (!nl) { nullable = false; break; }
+            }
+            break;
+        case Node::ALT:
+            nullable = false;
+            for (auto& k : n->kids) {
+                bool nl = false;
+                if (!first_list(k, out, nl)) return false;
+                nullable |= nl;
+            }
+            break;
+        case Node::GROUP: return first_list(n->kids[0], out, nullable);
+        case Node::REPEAT: {
+            bool nl = false;
+            if (!first_list(n->kids[0], out, nl)) return false;
+            nullable = nl || n->min == 0;
+            break;
+        }
+        default: nullable = true; break;   // anchors / lookarounds are zero-width
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out.size() <= kMaxFirst;
+}
+
 // Zero-width anchor every match of n must begin with: Node::BOS (\A), Node::BOL (^) or -1.
 static int lead_anchor(const Node* n) {
     while (n->kind == Node::GROUP) n = n->kids[0].get();
@@ -502,6 +578,8 @@ static int lead_anchor(const Node* n) {
         case Node::BOS: return Node::BOS;
         case Node::BOL: return Node::BOL;
         case Node::SEQ: return n->kids.empty() ? -1 : lead_anchor(n->kids[0].get());
+        // a repetition with at least one iteration begins with its first iteration
+        case Node::REPEAT: return n->min >= 1 ? lead_anchor(n->kids[0].get()) : -1;
         case Node::ALT: {
             int a = -2;
             for (auto& k : n->kids) {
@@ -534,6 +612,12 @@ Regex::Regex(const std::string& utf8, int flags) {
         has_first_ = true;
         for (int c = 0; c < 128; ++c) first_[c] = set[c] ? 1 : 0;
         first_nonascii_ = nonascii;
+        std::vector<char32_t> list;
+        bool nl = false;
+        if (first_list(root_, list, nl) && !nl && !list.empty()) {
+            n_first_list_ = (int)list.size();
+            std::copy(list.begin(), list.end(), first_list_);
+        }
     }
 }
 
@@ -543,21 +627,30 @@ bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
     size_t e = 0;
     end.out = &e;
     Matcher mt{s, caps};
-    for (size_t pos = start; pos <= s.size(); ++pos) {
+    const char32_t* p = s.data();
+    const size_t n = s.size();
+    auto first_ok = [&](char32_t c) { return c < 128 ? first_[c] != 0 : first_nonascii_; };
+    for (size_t pos = start; pos <= n; ++pos) {
         if (anchored_ && pos > 0) return false;
-        if (line_anchored_ && pos > 0 && s[pos - 1] != '\n') {
-            // next line start: the character after the next '\n'
-            size_t q = pos;
-            while (q < s.size() && s[q - 1] != '\n') ++q;
-            if (q >= s.size() && !(q == s.size() && s[q - 1] == '\n')) return false;
-            pos = q;
-        }
-        if (has_first_) {
+        if (line_anchored_) {
+            if (pos > 0 && p[pos - 1] != '\n') {   // next line start: the character after the next '\n'
+                const size_t j = scan::find_char(p, pos, n, U'\n');
+                if (j >= n) return false;
+                pos = j + 1;
+            }
+            // a match starts with one of the first characters: else try the next line
+            if (has_first_ && (pos == n || !first_ok(p[pos]))) {
+                if (pos == n) return false;
+                continue;
+            }
+        } else if (has_first_) {
             // skip to the next character a match can start with
-            const size_t n = s.size();
-            while (pos < n && !(s[pos] < 128 ? first_[s[pos]] : first_nonascii_)) ++pos;
+            if (n_first_list_) {
+                pos = scan::find_any(p, pos, n, first_list_, n_first_list_);
+            } else {
+                while (pos < n && !first_ok(p[pos])) ++pos;
+            }
             if (pos == n) return false;
-            if (line_anchored_ && pos > 0 && s[pos - 1] != '\n') continue;
         }
         if (mt.m(root_.get(), pos, end)) {
             caps[0] = (long)pos;

@@ -73,10 +73,13 @@ private:
     bool has_first_ = false;          // first-character filter active
     uint8_t first_[128] = {};         // ASCII characters a match can start with
     bool first_nonascii_ = true;      // ... and whether any non-ASCII one can
+    char32_t first_list_[8] = {};     // the exact first-character set when it is this small
+    int n_first_list_ = 0;            // (vector scan; 0: use first_)
     friend struct Matcher;
 };
 
 Str from_utf8(const std::string& s);
+Str from_utf8(const char* data, size_t n);
 std::string to_utf8(const Str& s);
 
 // \b / \w word characters: ASCII [A-Za-z0-9_] plus the installed non-ASCII ranges (Python's

@@ -165,6 +165,38 @@ def test_batch_prep_matches_python(hp):
         assert ex[i] == (keys.index(e.key) if e is not None else -1), i
 
 
+def test_wordset_token_fuzz(hp):
+    """The wordset scan (content_helper.rb:109, (?:[\\w/-](?:'s|(?<=s)')?)+) on texts dense in its
+    corner cases: apostrophes after 's' and before 's' (including "it's'" where the 's' taken by
+    's gets no s' of its own), doubled quotes, '/' and '-' inside and around tokens, tokens and
+    runs longer than the native scan's 64-character blocks, vocabulary and non-vocabulary words."""
+    rng = random.Random(11)
+    vocab = hp.corpus.vocab
+    pieces = ["it's'", "users'", "s''s", "'s", "s'", "x's's", "don't", "a/b-c", "--", "//", "-x-", "s's'",
+              "q'", "'", "''", "/'s", "-'", "_'s_"]
+    texts = []
+    for i in range(300):
+        toks = []
+        for _ in range(rng.randint(1, 80)):
+            r = rng.random()
+            if r < 0.4:
+                toks.append(rng.choice(vocab))
+            elif r < 0.7:
+                toks.append(rng.choice(pieces))
+            elif r < 0.8:
+                toks.append(''.join(rng.choice('abs-/_\'') for _ in range(rng.randint(60, 140))))
+            else:
+                toks.append(rng.choice(vocab) + rng.choice(pieces) + rng.choice(vocab))
+        texts.append(''.join(rng.choice([' ', '\n', ', ', '.']) + t for t in toks))
+    fb, cr, ex, fell = hp.prep_files(texts, ['LICENSE'] * len(texts), nthreads=2)
+    assert not fell.any()
+    corpus = hp.corpus
+    for i, t in enumerate(texts):
+        lf = LicenseFile(t, 'LICENSE')
+        bits, wf = corpus.intern(lf.wordset())
+        assert fb.wordset_size[i] == wf and np.array_equal(fb.bits[i], bits), (i, t[:200])
+
+
 def test_thousands_of_copyright_lines(hp):
     """A file opening with ~10k consecutive copyright lines (the copyright pattern's repeated
     group, content_helper.rb:255 + copyright.rb:8-11, nests the backtracking matcher once per

@@ -1,7 +1,8 @@
 """The native host library under AddressSanitizer + UndefinedBehaviorSanitizer.
 
 tests/sanitize/driver.cpp links csrc/rx.cpp, normalize.cpp and vocab_pack.cpp built with
--fsanitize=address,undefined (no recovery) and drives every entry point of
+-fsanitize=address,undefined (no recovery), once for baseline x86-64 (the scalar scans) and once
+for x86-64-v3 (the AVX2 scans of csrc/scan.h, as the shipped library is built), and drives every entry point of
 include/licensee_host.h -- lh_create, lh_set_unicode, lh_set_templates, threaded
 lh_prep_files, lh_normalize, lh_vocab_pack, lh_destroy -- over the reference fixture texts
 (goldens), all 47 template texts, seeded fuzz texts (markup, non-ASCII, contextual
@@ -55,7 +56,8 @@ def _texts():
 
 
 @pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
-def test_host_library_under_asan_ubsan(tmp_path):
+@pytest.mark.parametrize('march', ['x86-64', 'x86-64-v3'])   # scalar scans / the AVX2 scans (scan.h)
+def test_host_library_under_asan_ubsan(tmp_path, march):
     from licensee_amd import content_helper as ch
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.license import License
@@ -83,7 +85,7 @@ def test_host_library_under_asan_ubsan(tmp_path):
     inp.write_bytes(blob)
     exe = str(tmp_path / 'drv')
     csrc = os.path.join(ROOT, 'licensee_amd', 'csrc')
-    subprocess.run(['g++', '-std=c++17', '-O1', '-g', '-fno-omit-frame-pointer', '-fsanitize=address,undefined',
+    subprocess.run(['g++', '-std=c++17', '-O1', '-g', f'-march={march}', '-fno-omit-frame-pointer', '-fsanitize=address,undefined',
                     '-fno-sanitize-recover=all', '-pthread', '-I', os.path.join(ROOT, 'include'), '-I', csrc,
                     '-o', exe, os.path.join(HERE, 'sanitize', 'driver.cpp'), os.path.join(csrc, 'rx.cpp'),
                     os.path.join(csrc, 'normalize.cpp'), os.path.join(csrc, 'vocab_pack.cpp')], check=True)

@@ -1,0 +1,60 @@
+"""Per-pass timing of the native host preparation (csrc/normalize.cpp built with -DLH_PASS_TIMING).
+
+    python tools/host_prep_passes.py [n_texts] [threads]
+
+Builds a diagnostic copy of liblicensee_host.so under /tmp, points licensee_amd.native_host at
+it, prepares n synthetic config-2 texts (SyntheticCorpus.text, ~9 KB each) and prints the
+seconds spent in every pass (summed over threads) and the batch rate.
+"""
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    threads = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    march = os.environ.get('LH_MARCH', 'x86-64-v3')
+    csrc = os.path.join(ROOT, 'licensee_amd', 'csrc')
+    so = '/tmp/liblicensee_host_timing.so'
+    subprocess.run(['g++', '-O3', f'-march={march}', '-std=c++17', '-fPIC', '-shared', '-pthread', '-DLH_PASS_TIMING', '-o', so] +
+                   [os.path.join(csrc, f) for f in ('rx.cpp', 'normalize.cpp', 'vocab_pack.cpp')], check=True)
+    import ctypes
+    from licensee_amd import native_host
+    native_host.LIB_PATH = so
+    lib = native_host._load()
+    lib.lh_pass_timing.restype = ctypes.c_int64
+    lib.lh_pass_timing.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from licensee_amd.synth import SyntheticCorpus
+    corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    syn = SyntheticCorpus(corpus)
+    texts = [syn.text(i)[0] for i in range(n)]
+    hp = native_host.HostPrep(corpus)
+    hp.prep_files(texts[:50], None, nthreads=threads)
+    best = None
+    for _ in range(3):   # the best of 3 runs (shared machines are noisy)
+        lib.lh_pass_timing(None, 0)
+        t0 = time.perf_counter()
+        hp.prep_files(texts, None, nthreads=threads)
+        wall = time.perf_counter() - t0
+        buf = ctypes.create_string_buffer(1 << 16)
+        lib.lh_pass_timing(buf, 1 << 16)
+        if best is None or wall < best[0]:
+            best = (wall, buf.value.decode())
+    wall = best[0]
+    rows = [(l.split()[0], float(l.split()[1])) for l in best[1].splitlines()]
+    tot = sum(s for _, s in rows)
+    print(f'{n} texts ({sum(map(len, texts)) / n / 1024:.1f} KiB avg), {threads} threads: {wall:.3f} s wall, '
+          f'{n / wall:.0f} files/s; passes sum {tot:.3f} s')
+    for name, sec in sorted(rows, key=lambda r: -r[1]):
+        print(f'  {name:20s} {sec:8.4f} s  {100 * sec / tot:5.1f}%  {sec / n * 1e6:8.1f} us/file')
+
+
+if __name__ == '__main__':
+    main()
