@@ -200,8 +200,10 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
 // template masks are wave-uniform scalar loads, the next template's issued before this one is
 // scored. Partial overlaps go to an LDS [file][template] u16 stage (row stride tp + 2 halves:
 // an odd number of dwords, so the 64 lanes hit 64 banks), then out as row-major [n][tp] u16.
+// Occupancy: two workgroups per CU (8 waves per SIMD) while the stage fits twice in LDS
+// (TPMAX 608); one at the 704 maximum.
 template <int DP, int TPMAX>
-__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_dense(
+__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(TPMAX <= 608 ? 8 : 4, TPMAX <= 608 ? 8 : 4))) void dice_post_dense(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint64_t* __restrict__ dmask, uint16_t* __restrict__ dense) {
     __shared__ uint32_t stage32[kPostFiles * (TPMAX + 2) / 2];   // <= 78 KiB at TPMAX 608: 2 per CU

@@ -177,8 +177,12 @@ constexpr struct ByteMasks {
 } kByteMasks;
 
 inline uint64_t key_mix(uint64_t lo, uint64_t hi, uint64_t len, uint64_t tail) {
-    uint64_t h = (lo ^ (hi * 0xC2B2AE3D27D4EB4FULL) ^ (len << 56) ^ tail) * 0x9E3779B97F4A7C15ULL;
-    return h ^ (h >> 29);
+    uint64_t h = lo ^ (hi * 0xC2B2AE3D27D4EB4FULL) ^ (len << 56) ^ tail;
+    h ^= h >> 33;   // fmix64: every output bit depends on every input bit (slots are low bits)
+    h *= 0xFF51AFD7ED558CCDULL;
+    h ^= h >> 33;
+    h *= 0xC4CEB9FE1A85EC53ULL;
+    return h ^ (h >> 33);
 }
 
 template <class C>
@@ -237,60 +241,69 @@ inline bool tail_equal(const std::string& w, const char32_t* p) {
     return true;
 }
 
-// The template vocabulary: open addressing over packed word keys, words kept for the tail
-// compare of long words.
+// The template vocabulary: open addressing over 32-bit slots (id + 1 in the low id_bits, a
+// hash tag above; 0 = empty) small enough to stay in L1, the packed keys in id order for the
+// compare; words kept for the tail compare of long words.
 struct VocabTable {
-    struct Slot {
+    struct Key {
         uint64_t lo, hi;
         uint32_t len;
-        int32_t id;   // -1: empty
     };
-    std::vector<Slot> slot;
+    std::vector<uint32_t> slot;
+    std::vector<Key> key;
     std::vector<std::string> words;
     uint64_t mask = 0;
+    int id_bits = 1;
+    uint32_t id_mask = 1;
+    uint32_t tag(uint64_t h) const { return (uint32_t)(h >> 40) << id_bits; }
     void build(int32_t n, const char* const* vocab) {
         size_t cap = 16;
         while (cap < 2 * (size_t)n + 1) cap <<= 1;
-        slot.assign(cap, Slot{0, 0, 0, -1});
+        id_bits = 1;
+        while (((uint64_t)1 << id_bits) <= (uint64_t)n + 1) ++id_bits;
+        if (id_bits > 28) throw std::runtime_error("vocabulary too large for the host word table");
+        id_mask = (1u << id_bits) - 1;
+        slot.assign(cap, 0);
+        key.resize((size_t)n);
         mask = cap - 1;
         words.assign(vocab, vocab + n);
         for (int32_t i = 0; i < n; ++i) {
             const WordKey k = word_key(words[i]);
+            key[(size_t)i] = Key{k.lo, k.hi, k.len};
             size_t j = k.h & mask;
-            while (slot[j].id >= 0) j = (j + 1) & mask;
-            slot[j] = Slot{k.lo, k.hi, k.len, i};
+            while (slot[j]) j = (j + 1) & mask;
+            slot[j] = tag(k.h) | (uint32_t)(i + 1);
         }
     }
     int32_t find(const WordKey& k, const char32_t* p) const {
         if (slot.empty()) return -1;
+        const uint32_t t = tag(k.h);
         for (size_t j = k.h & mask;; j = (j + 1) & mask) {
-            const Slot& s = slot[j];
-            if (s.id < 0) return -1;
-            if (s.lo == k.lo && s.hi == k.hi && s.len == k.len && (k.len <= 16 || tail_equal(words[(size_t)s.id], p)))
-                return s.id;
+            const uint32_t s = slot[j];
+            if (!s) return -1;
+            if ((s & ~id_mask) != t) continue;
+            const int32_t id = (int32_t)(s & id_mask) - 1;
+            const Key& e = key[(size_t)id];
+            if (e.lo == k.lo && e.hi == k.hi && e.len == k.len && (k.len <= 16 || tail_equal(words[(size_t)id], p)))
+                return id;
         }
     }
 };
 
 // A file's distinct non-vocabulary words: open addressing over packed keys (start, len into
 // the text for the tail compare), reused by a thread across files (an epoch stamp marks the
-// live slots, so nothing is cleared per file).
+// live slots, so nothing is cleared per file); doubles when half full.
 struct WordSet {
     struct Slot {
         uint64_t lo, hi;
-        uint32_t start, len, epoch;
+        uint32_t start, len, epoch, hash;
     };
     std::vector<Slot> slot;
     uint32_t cur = 0;
     size_t count = 0, mask = 0;
     const Str* text = nullptr;
     void reset(const Str& s) {
-        size_t need = 16;
-        while (need < s.size() + 32) need <<= 1;   // distinct words <= chars / 2 + 1: load <= 1/2
-        if (need > slot.size()) {
-            slot.assign(need, Slot{0, 0, 0, 0, 0});
-            cur = 0;
-        }
+        if (slot.empty()) slot.assign(1024, Slot{0, 0, 0, 0, 0, 0});
         mask = slot.size() - 1;
         if (++cur == 0) {   // epoch wrapped: clear once
             for (auto& e : slot) e.epoch = 0;
@@ -299,13 +312,25 @@ struct WordSet {
         count = 0;
         text = &s;
     }
+    void grow() {
+        std::vector<Slot> old;
+        old.swap(slot);
+        slot.assign(old.size() * 2, Slot{0, 0, 0, 0, 0, 0});
+        mask = slot.size() - 1;
+        for (const Slot& e : old) {
+            if (e.epoch != cur) continue;
+            size_t j = e.hash & mask;
+            while (slot[j].epoch == cur) j = (j + 1) & mask;
+            slot[j] = e;
+        }
+    }
     // true when the token [a, a + k.len) is a new word
     bool insert(size_t a, const WordKey& k) {
         for (size_t j = k.h & mask;; j = (j + 1) & mask) {
             Slot& s = slot[j];
             if (s.epoch != cur) {
-                s = Slot{k.lo, k.hi, (uint32_t)a, k.len, cur};
-                ++count;
+                s = Slot{k.lo, k.hi, (uint32_t)a, k.len, cur, (uint32_t)k.h};
+                if (2 * ++count > slot.size()) grow();
                 return true;
             }
             if (s.lo == k.lo && s.hi == k.hi && s.len == k.len &&
@@ -390,26 +415,30 @@ struct Normalizer {
         std::vector<long> caps;
         while (t.search(cur, 0, caps)) strip_re(t);
     }
+    // strip_comments (content_helper.rb:263-267): when every line of String#split("\n") (trailing
+    // empty fields dropped) matches comment_markup ^[ \t\n\v\f\r]*?[/*]{1,2} -- on a line: its
+    // first character outside [ \t\v\f\r] is '/' or '*' -- and there is not exactly one line
+    static bool comment_line(const char32_t* p, size_t a, size_t b) {
+        while (a < b && (p[a] == ' ' || p[a] == '\t' || p[a] == '\v' || p[a] == '\f' || p[a] == '\r')) ++a;
+        return a < b && (p[a] == '/' || p[a] == '*');
+    }
     void strip_comments() {
-        // String#split("\n") drops trailing empty fields
-        std::vector<Str> lines;
-        size_t a = 0;
-        for (size_t i = 0; i <= cur.size(); ++i) {
-            if (i == cur.size() || cur[i] == '\n') { lines.push_back(cur.substr(a, i - a)); a = i + 1; }
+        const char32_t* p = cur.data();
+        size_t end = cur.size();
+        while (end > 0 && p[end - 1] == '\n') --end;   // trailing empty fields
+        if (end > 0 && scan::find_char(p, 0, end, U'\n') == end) return;   // one line
+        for (size_t a = 0; a < end;) {
+            const size_t e = scan::find_char(p, a, end, U'\n');
+            if (!comment_line(p, a, e)) return;
+            a = e + 1;
         }
-        while (!lines.empty() && lines.back().empty()) lines.pop_back();
-        if (lines.size() == 1) return;
-        std::vector<long> caps;
-        const Regex& cm = c.R("comment_markup");
-        for (auto& l : lines)
-            if (!cm.search(l, 0, caps)) return;
-        strip_re(cm);
+        strip_re(c.R("comment_markup"));
     }
 
     // hyphenated (content_helper.rb:40) can only match a '-' followed by [ \t\v\f\r]* and '\n'
     static bool has_hyphen_break(const Str& s) {
-        for (size_t i = 0; i < s.size(); ++i) {
-            if (s[i] != '-') continue;
+        for (size_t i = scan::find_char(s.data(), 0, s.size(), U'-'); i < s.size();
+             i = scan::find_char(s.data(), i + 1, s.size(), U'-')) {
             size_t j = i + 1;
             while (j < s.size() && (s[j] == ' ' || s[j] == '\t' || s[j] == '\v' || s[j] == '\f' || s[j] == '\r')) ++j;
             if (j < s.size() && s[j] == '\n') return true;
@@ -496,6 +525,32 @@ struct Normalizer {
         return (c.spell_tok[h >> 6] >> (h & 63)) & 1;
     }
 
+    // Vector part of the downcase/quote pass: 8-character blocks of ASCII only are downcased,
+    // '"' and '`' become '\'', and '&' are counted; stops at the first block holding a non-ASCII
+    // character (ascii_done_: where the scalar loop continues).
+    size_t ascii_done_ = 0;
+    void downcase_quote_ascii(size_t& amps) {
+        size_t i = 0;
+#if defined(__AVX2__)
+        char32_t* p = cur.data();
+        const size_t n = cur.size();
+        const __m256i A1 = _mm256_set1_epi32('A' - 1), Z1 = _mm256_set1_epi32('Z' + 1), c32 = _mm256_set1_epi32(32);
+        const __m256i dq = _mm256_set1_epi32('"'), bt = _mm256_set1_epi32('`'), sq = _mm256_set1_epi32('\'');
+        const __m256i amp = _mm256_set1_epi32('&'), c127 = _mm256_set1_epi32(127);
+        for (; i + 8 <= n; i += 8) {
+            __m256i v = _mm256_loadu_si256((const __m256i*)(p + i));
+            if (scan::lanes(_mm256_cmpgt_epi32(v, c127))) break;
+            const __m256i up = _mm256_and_si256(_mm256_cmpgt_epi32(v, A1), _mm256_cmpgt_epi32(Z1, v));
+            v = _mm256_add_epi32(v, _mm256_and_si256(up, c32));
+            v = _mm256_blendv_epi8(v, sq, _mm256_or_si256(_mm256_cmpeq_epi32(v, dq), _mm256_cmpeq_epi32(v, bt)));
+            amps += (size_t)__builtin_popcount(scan::lanes(_mm256_cmpeq_epi32(v, amp)));
+            _mm256_storeu_si256((__m256i*)(p + i), v);
+        }
+#endif
+        (void)amps;
+        ascii_done_ = i;
+    }
+
     // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip, in place
     void collapse_whitespace() {
         cur.resize(scan::squeeze_runs(cur.data(), 0, 0, cur.size(), false, true));
@@ -518,7 +573,9 @@ struct Normalizer {
         // quote characters -> "'" (content_helper.rb:34-41), one pass
         PASS("downcase_amp_quote", {
             size_t amps = 0;
-            for (auto& ch : cur) {
+            downcase_quote_ascii(amps);
+            for (size_t i = ascii_done_; i < cur.size(); ++i) {
+                char32_t& ch = cur[i];
                 if (ch < 128) {
                     if (ch >= 'A' && ch <= 'Z') ch += 32;
                     else if (ch == '"' || ch == '`') ch = '\'';
@@ -561,10 +618,9 @@ struct Normalizer {
         // (?<!^)([\u2014\u2013-]+)(?!$) -> '-' changes nothing unless a run holds an em/en dash or
         // two hyphens: skip the regex when the text has neither
         PASS("dashes", {
-            bool may = false;
-            for (size_t i = 0; i < cur.size() && !may; ++i)
-                may = cur[i] == 0x2014 || cur[i] == 0x2013 || (cur[i] == '-' && i + 1 < cur.size() && cur[i + 1] == '-');
-            if (may) sub_re(c.R("dashes"), U"-");
+            static const char32_t kDash[2] = {0x2014, 0x2013};
+            if (scan::find_any(cur.data(), 0, cur.size(), kDash, 2) < cur.size() || contains(cur, U"--"))
+                sub_re(c.R("dashes"), U"-");
         });
         PASS("hyphenated", if (has_hyphen_break(cur)) sub_re(c.R("hyphenated"), U"\\1-\\2"));
         PASS("spelling", spelling());
@@ -893,20 +949,15 @@ int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t
                 // others through the per-thread WordSet
                 WordSet& words = tl_words;
                 words.reset(o.normalized);
-                size_t n_vocab_words = 0;
                 PASS("wordset", scan_words(o.normalized, [&](size_t a, size_t b) {
                     const char32_t* p = o.normalized.data() + a;
                     const WordKey k = word_key(p, b - a, o.normalized.size() - a);
                     const int32_t id = c->vocab.find(k, p);
-                    if (id >= 0) {
-                        uint64_t& wd = row[(size_t)id >> 6];
-                        const uint64_t bit = 1ULL << (id & 63);
-                        n_vocab_words += (wd & bit) == 0;
-                        wd |= bit;
-                    } else {
-                        words.insert(a, k);
-                    }
+                    if (id >= 0) row[(size_t)id >> 6] |= 1ULL << (id & 63);
+                    else words.insert(a, k);
                 }));
+                size_t n_vocab_words = 0;
+                for (uint64_t wd : row) n_vocab_words += (size_t)__builtin_popcountll(wd);
                 const size_t n_words = n_vocab_words + words.count;
                 memcpy(bits + (size_t)f * c->w64, row.data(), sizeof(uint64_t) * (size_t)c->w64);
                 wf[f] = (uint32_t)n_words;

@@ -380,10 +380,19 @@ struct Matcher {
                 return a != b && k(pos);
             }
             case Node::SEQ: return seq(n, 0, pos, k);
-            case Node::ALT:
-                for (auto& kid : n->kids)
-                    if (m(kid.get(), pos, k)) return true;
+            case Node::ALT: {
+                // branches that cannot start with s[pos] are skipped (first-character masks)
+                const char32_t c = pos < s.size() ? s[pos] : 0;
+                const bool end = pos >= s.size();
+                for (size_t i = 0; i < n->kids.size(); ++i) {
+                    if (!n->alt_nullable[i]) {
+                        if (end) continue;
+                        if (c < 128 ? !(n->alt_first[2 * i + (c >> 6)] >> (c & 63) & 1) : !n->alt_nonascii[i]) continue;
+                    }
+                    if (m(n->kids[i].get(), pos, k)) return true;
+                }
                 return false;
+            }
             case Node::GROUP: {
                 if (n->group < 0) return m(n->kids[0].get(), pos, k);
                 const long o0 = caps[2 * n->group], o1 = caps[2 * n->group + 1];
@@ -519,6 +528,25 @@ static void first_chars(const NodeP& n, std::vector<bool>& set, bool& nonascii, 
     }
 }
 
+// Fill every ALT node's per-branch first-character masks (Node::alt_first).
+static void index_alternations(const NodeP& n) {
+    for (auto& k : n->kids) index_alternations(k);
+    if (n->kind != Node::ALT) return;
+    const size_t nb = n->kids.size();
+    n->alt_first.assign(2 * nb, 0);
+    n->alt_nonascii.assign(nb, 0);
+    n->alt_nullable.assign(nb, 0);
+    for (size_t i = 0; i < nb; ++i) {
+        std::vector<bool> set(128, false);
+        bool nonascii = false, nullable = false;
+        first_chars(n->kids[i], set, nonascii, nullable);
+        for (int c = 0; c < 128; ++c)
+            if (set[c]) n->alt_first[2 * i + (c >> 6)] |= 1ull << (c & 63);
+        n->alt_nonascii[i] = nonascii;
+        n->alt_nullable[i] = nullable;
+    }
+}
+
 // The exact set of code points a match of n can start with, when it has at most kMaxFirst
 // members (false otherwise, or when n can match empty: nullable).
 static constexpr size_t kMaxFirst = 8;
@@ -600,6 +628,7 @@ Regex::Regex(const std::string& utf8, int flags) {
     root_ = ps.parse_alt((flags & IGNORECASE) != 0, (flags & DOTALL) != 0);
     if (!ps.eof()) throw std::runtime_error("rx parse: unbalanced )");
     ngroups_ = ps.ngroups;
+    index_alternations(root_);
     // Where a match can start: \A-led patterns only at position 0, ^-led patterns only at line
     // starts (every pattern here is re.M). An alternation qualifies when all its branches do.
     const int lead = lead_anchor(root_.get());

@@ -47,6 +47,10 @@ struct Node {
     int min = 0, max = -1;                          // REPEAT (-1: unbounded)
     bool lazy = false;                              // REPEAT
     int width = -1;                                 // LOOK (behind): fixed width
+    // ALT: per branch, the ASCII characters it can start with (bit c of first[2 * i + c / 64]),
+    // whether it can start with a non-ASCII one, whether it can match empty (then never skipped)
+    std::vector<uint64_t> alt_first;
+    std::vector<uint8_t> alt_nonascii, alt_nullable;
 };
 
 class Regex {

@@ -3,7 +3,7 @@
     python tools/host_prep_passes.py [n_texts] [threads]
 
 Builds a diagnostic copy of liblicensee_host.so under /tmp, points licensee_amd.native_host at
-it, prepares n synthetic config-2 texts (SyntheticCorpus.text, ~9 KB each) and prints the
+it, prepares n synthetic config-2 texts (SyntheticCorpus.text, ~9 KB each, as UTF-8 bytes) and prints the
 seconds spent in every pass (summed over threads) and the batch rate.
 """
 import os
@@ -34,7 +34,7 @@ def main():
     from licensee_amd.synth import SyntheticCorpus
     corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
     syn = SyntheticCorpus(corpus)
-    texts = [syn.text(i)[0] for i in range(n)]
+    texts = [syn.text(i)[0].encode('utf-8') for i in range(n)]   # file contents as bytes, as bench.py
     hp = native_host.HostPrep(corpus)
     hp.prep_files(texts[:50], None, nthreads=threads)
     best = None
