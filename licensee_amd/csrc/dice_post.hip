@@ -13,19 +13,24 @@
 // (in hundreds of templates) stay bitset-scored: the vocabulary's first D u64 words (the host
 // packs the widest words first) are ANDed against dense template masks.
 //
-// One workgroup = 16 waves = one tile of 64 files:
-//   phase 1 (dense prefix, lanes = files): wave w scores templates [w*TW, (w+1)*TW) over the
-//            files' first D u64 words (template masks uniform: scalar loads), writing the
-//            partial overlaps to a u16 counter matrix in LDS, [file][template] (row stride
-//            tpad + 2 halves: conflict-free for both access patterns below);
-//   phase 2 (narrow words, one file per wave): lanes read the file's remaining u64 words; each
-//            set bit is a word whose postings rows (16 template ids per row, 0xFFFF padding)
-//            are queued in a per-wave LDS list; a group of 16 lanes walks one queued word's
-//            rows and adds 1 to each listed template's counter (ds_add_u32 on the u16 pair);
-//   phase 3 (score, lanes = templates): t = lane + 64 j: overlap from LDS, denominator from
-//            the template constants, running best per lane, then a wave reduction (the same
-//            strict order as every other kernel: score, then later key); the matrix mode
-//            writes the row-major [n][T] row and the top-k.
+// Two kernels per launch, each workgroup = 16 waves over one tile of 64 files:
+//   dice_post_dense (lanes = files): wave w scores templates [w*TW, (w+1)*TW) over the files'
+//            first D u64 words (template masks wave-uniform: scalar loads) into an LDS
+//            [file][template] u16 stage, written out as a row-major [n][tp] u16 matrix
+//            (2 workgroups per CU while the stage fits twice in LDS);
+//   dice_post_narrow_{match,matrix} (one file per wave): the file's dense partials, widened,
+//            start the wave's u32 counter row in LDS; its remaining u64 words are loaded
+//            kChunks x 64 at a time and their set bits (narrow words) are queued in a per-wave
+//            LDS list, slots assigned by a DPP wave prefix sum; walk_short gives each queued
+//            word one lane, reads its 32-byte postings row (16 entries, each a byte offset
+//            4*t into the counter row, 0xFFFF padding) and adds 1 to the first 8 listed
+//            counters (ds_add_u32); words with 9-16 entries wait in a mid queue (entries 8-15),
+//            longer ones in a long queue walked by all 64 lanes from the plong array. Scoring
+//            reads (and re-zeroes) the row with lanes = templates (t = lane + 64 j), using the
+//            packed template constants {len | cc << 31, base | slack << 16}: the same
+//            denominator, IEEE score and strict order (score, then later key) as every other
+//            kernel, 24-bit exact compares inside the fast envelope; match mode reduces over
+//            the wave, matrix mode writes the row-major [n][T] row and a k-round top-k.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -119,6 +119,27 @@ def test_vendored_properties_batched_on_gpu():
         assert (got == keys[i]) == expect[i], (keys[i], i, got)
 
 
+def test_vendored_confidence_equals_similarity():
+    """vendored_license_spec.rb:27-29: for every vendored license rendered with copyright info,
+    LicenseFile#confidence == License#similarity(license_file) -- the confidence from the
+    matcher chain (Exact, else Dice's batched GPU match) and the similarity from the GPU pair
+    path, both equal to the oracle's Set#& restatement (content_helper.rb:128-133)."""
+    from oracle import dice_oracle as O
+    from tests.helpers import oracle_templates
+    licenses = License.all(hidden=True, pseudo=False)
+    otpl = {t.key: t for t in oracle_templates(licenses)}
+    n = 0
+    for t in golden('vendored.json')['templates']:
+        rec = t['cases']['rendered']
+        f = GoldenLicenseFile(rec)
+        lic = License.find(t['key'])
+        conf, sim = f.confidence(), lic.similarity(f)
+        assert conf == sim, (t['key'], conf, sim)
+        assert sim == O.similarity(otpl[t['key']], O.OracleFile(rec['normalized'])), t['key']
+        n += 1
+    assert n == len(licenses)
+
+
 @pytest.fixture(scope='module')
 def big():
     from licensee_amd._native import Scorer

@@ -21,15 +21,30 @@ def main():
     src, tag, config, files, templates = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_stats.csv'))))
-    # the product kernel of the timed region (copies/packing outside it are listed, not chosen)
-    product = [r for r in stats if r['Name'].replace('void ', '').startswith(('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice::dice_lds_'))]
-    top = max(product or stats, key=lambda r: float(r['TotalDurationNs']))
-    kernel = top['Name'].split('(')[0].replace('void ', '')
-    avg_ns = float(top['AverageNs'])
-    fetch = load_counters(os.path.join(src, 'fetch', 'run_counter_collection.csv'), kernel)
-    write = load_counters(os.path.join(src, 'write', 'run_counter_collection.csv'), kernel)
-    sq = load_counters(os.path.join(src, 'sq', 'run_counter_collection.csv'), kernel)
-    clk = load_counters(os.path.join(src, 'clk', 'run_counter_collection.csv'), kernel)
+    # the product kernels of the timed region (copies/packing outside it are listed, not chosen):
+    # the sparse program / dense / LDS kernels run one launch per step, the postings path two
+    # (dice_post_dense + dice_post_narrow_*): a step's time and traffic sum over them
+    prefixes = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_')
+    def base(r):
+        return r['Name'].split('(')[0].replace('void ', '').replace('dice::', '')
+    product = [r for r in stats if base(r).startswith(prefixes)]
+    if not product:
+        product = [max(stats, key=lambda r: float(r['TotalDurationNs']))]
+    top_calls = max(int(r['Calls']) for r in product)
+    product = [r for r in product if int(r['Calls']) == top_calls]
+    kernels = [r['Name'].split('(')[0].replace('void ', '') for r in product]
+    kernel = ' + '.join(kernels)
+    avg_ns = sum(float(r['AverageNs']) for r in product)
+    def summed(path):
+        out = collections.Counter()
+        for k in kernels:
+            for name, v in load_counters(path, k).items():
+                out[name] += v
+        return dict(out)
+    fetch = summed(os.path.join(src, 'fetch', 'run_counter_collection.csv'))
+    write = summed(os.path.join(src, 'write', 'run_counter_collection.csv'))
+    sq = summed(os.path.join(src, 'sq', 'run_counter_collection.csv'))
+    clk = summed(os.path.join(src, 'clk', 'run_counter_collection.csv'))
     # gfx950: FETCH_SIZE (KB) counts half the bytes of wide coalesced streaming reads -> x2
     # (MI355X_MICROARCH.md §HBM); WRITE_SIZE (KB) is exact for streaming stores.
     read_b = fetch.get('FETCH_SIZE', 0) * 1024 * 2
@@ -37,7 +52,8 @@ def main():
     hbm = read_b + write_b
     eff_clk = clk.get('GRBM_GUI_ACTIVE', 0) / 8 / (avg_ns * 1e-9) / 1e9 if avg_ns else 0
     pmc = {'tag': tag, 'config': config, 'kernel': kernel, 'files_per_launch': files, 'templates': templates,
-           'avg_kernel_ns': avg_ns, 'hbm_bytes_per_launch': hbm, 'read_bytes': read_b, 'write_bytes': write_b,
+           'avg_kernel_ns': avg_ns, 'per_kernel_avg_ns': {k: float(r['AverageNs']) for k, r in zip(kernels, product)},
+           'hbm_bytes_per_launch': hbm, 'read_bytes': read_b, 'write_bytes': write_b,
            'hbm_gbs': hbm / (avg_ns * 1e-9) / 1e9, 'effective_clock_ghz': eff_clk, 'sq': sq,
            'valu_busy_frac': sq.get('SQ_INSTS_VALU', 0) * 2 / 1024 / (clk.get('GRBM_GUI_ACTIVE', 1) / 8)}
     os.makedirs(os.path.join(root, 'profiles'), exist_ok=True)
@@ -49,7 +65,7 @@ def main():
         fh.write('## Kernel trace stats (`rocprofv3 --kernel-trace --stats`)\n\n| kernel | calls | avg ns | min ns | max ns | % |\n|---|---|---|---|---|---|\n')
         for r in stats:
             fh.write(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['AverageNs']):.0f} | {r['MinNs']} | {r['MaxNs']} | {float(r['Percentage']):.1f} |\n")
-        fh.write(f'\n## PMC (separate passes) for `{kernel}`, per launch\n\n')
+        fh.write(f'\n## PMC (separate passes) for `{kernel}`, per step (summed over these kernels)\n\n')
         fh.write(f'- FETCH_SIZE {fetch.get("FETCH_SIZE", 0):.0f} KB (x2 gfx950 correction) -> read {read_b / 1e6:.1f} MB\n')
         fh.write(f'- WRITE_SIZE {write.get("WRITE_SIZE", 0):.0f} KB -> write {write_b / 1e6:.1f} MB\n')
         fh.write(f'- HBM traffic {hbm / 1e6:.1f} MB per launch = {pmc["hbm_gbs"]:.0f} GB/s at the kernel average\n')
