@@ -149,6 +149,24 @@ def pack_vocabulary(order: List[str], members: Dict[str, List[int]], n_templates
     return [order[i] for i in perm]
 
 
+# The postings kernel (T > 64, csrc/dice_post.hip) scores the first D <= 16 u64 words of the
+# vocabulary as dense template masks and every later word through its postings list, whose
+# expected cost per file grows with the square of the list length: its widest words belong in
+# that prefix.
+_POSTINGS_PREFIX = 16 * 64
+
+
+def postings_prefix(order: List[str], members: Dict[str, List[int]]) -> List[str]:
+    """``order`` with its _POSTINGS_PREFIX widest words moved to the front, widest first (ties:
+    earlier in ``order``); the rest keep their relative order. Deterministic."""
+    if len(order) <= _POSTINGS_PREFIX:
+        return sorted(order, key=lambda w: -len(members[w]))   # stable: ties keep their order
+    pos = {w: i for i, w in enumerate(order)}
+    head = sorted(order, key=lambda w: (-len(members[w]), pos[w]))[:_POSTINGS_PREFIX]
+    chosen = set(head)
+    return head + [w for w in order if w not in chosen]
+
+
 def improve_packing(templates: Sequence, iters_per_word: int) -> Tuple[int, int]:
     """Build step: continue the local search from the cached order of ``templates``' corpus
     with a larger budget and keep the result when it is cheaper. Returns (old, new) cost."""
@@ -203,6 +221,8 @@ class TemplateCorpus:
             for w in lf:
                 members.setdefault(w, []).append(i)
         self.vocab: List[str] = pack_vocabulary(vocabulary_order(members, len(lfs)), members, len(lfs))
+        if len(lfs) > 64:
+            self.vocab = postings_prefix(self.vocab, members)
         self.index: Dict[str, int] = {w: i for i, w in enumerate(self.vocab)}
         V = max(len(self.vocab), 1)
         self.n_vocab = V

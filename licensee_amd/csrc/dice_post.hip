@@ -45,7 +45,7 @@ namespace dice {
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
-constexpr int kPostMaxDense = 16;        // dense prefix u64 words
+constexpr int kPostMaxDense = 16;        // dense prefix u64 words (20 / 24 measured slower at T = 600)
 constexpr int kRowW = 16;                // template ids per postings row
 constexpr int kWordCap = 192;            // per-wave queue of narrow word ids
 constexpr int kMidCap = 128;             // per-wave queue of words with 9-16 postings

@@ -171,6 +171,11 @@ def test_full_size_match_vs_oracle_sample(big):
     eb, eo, es = orc.match(fb.bits[idx], fb.wordset_size[idx], fb.length[idx], fb.cc_false_positive[idx], 98.0,
                            nthreads=16, mode=1)
     assert np.array_equal(best[idx], eb) and np.array_equal(ov[idx], eo) and np.array_equal(score[idx], es)
+    # and the independent hash-set Set#& restatement (no AND+popcount) on another 20k files
+    idx = np.sort(np.random.default_rng(2).choice(fb.n, 20_000, replace=False))
+    eb, eo, es = orc.match(fb.bits[idx], fb.wordset_size[idx], fb.length[idx], fb.cc_false_positive[idx], 98.0,
+                           nthreads=16, mode=0)
+    assert np.array_equal(best[idx], eb) and np.array_equal(ov[idx], eo) and np.array_equal(score[idx], es)
     assert ((best >= 0) == (score >= 98.0)).all()
     assert best.min() >= -1 and best.max() < len(corpus.templates)
 
