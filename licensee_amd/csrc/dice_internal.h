@@ -59,7 +59,6 @@ struct dice_ctx {
     void* d_ptc = nullptr;     // [T] int4 template constants
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0;
     bool post_fast = false;
-    bool post_fused = false;   // match mode through dice_post_fused_match (DICE_POST_FUSED)
     int64_t post_rows = 0;
 };
 

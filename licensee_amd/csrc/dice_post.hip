@@ -101,20 +101,12 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
 }
 
-// Postings entries are byte offsets (4 * template) into the wave's u32 counter row. The fused
-// kernel keeps u16 counters (template t at byte 2 t): the same entry addresses the u32 pair
-// holding t's half at byte (e >> 1) & ~3, and the add is 1 << 16 for an odd t. No half can carry
-// into the other: a counter never exceeds its template's |Lf| < 65535 (post_feasible).
-template <bool k16>
-__device__ __forceinline__ void count(uint32_t* crow32, uint32_t e) {
-    if (k16)
-        atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(crow32) + ((e >> 1) & ~3u)), 1u << ((e & 4u) << 2));
-    else
-        atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(crow32) + e), 1u);
+// Postings entries are byte offsets (4 * template) into the wave's u32 counter row.
+__device__ __forceinline__ void count(uint32_t* crow32, uint32_t off) {
+    atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(crow32) + off), 1u);
 }
 
 // Long words (> 16 narrow postings): 64 lanes per word, 4 words' id loads in flight.
-template <bool k16>
 __device__ __forceinline__ void walk_long(const uint2* lq, uint32_t& nl, const uint16_t* __restrict__ plong,
                                           uint32_t* crow32, int lane) {
     constexpr int kB = 4;   // words whose id loads are in flight together
@@ -128,16 +120,15 @@ __device__ __forceinline__ void walk_long(const uint2* lq, uint32_t& nl, const u
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            if (id[u] != kNoTpl) count<k16>(crow32, id[u]);
+            if (id[u] != kNoTpl) count(crow32, id[u]);
             for (uint32_t r = kWave; r < q[u].y; r += kWave)   // > 64 postings (rare)
-                if (r + lane < q[u].y) count<k16>(crow32, plong[(int64_t)q[u].x + r + lane]);
+                if (r + lane < q[u].y) count(crow32, plong[(int64_t)q[u].x + r + lane]);
         }
     }
     nl = 0;
 }
 
 // Second halves (entries 8-15) of the queued MID words (9-16 postings), one lane per word.
-template <bool k16>
 __device__ __forceinline__ void walk_mid(const uint32_t* mq, uint32_t& nm, const uint16_t* __restrict__ prow,
                                          uint32_t* crow32, int lane) {
     for (uint32_t e0 = 0; e0 < nm; e0 += kWave) {
@@ -148,7 +139,7 @@ __device__ __forceinline__ void walk_mid(const uint32_t* mq, uint32_t& nm, const
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint32_t id = (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-            if (id < kMore) count<k16>(crow32, id);
+            if (id < kMore) count(crow32, id);
         }
     }
     nm = 0;
@@ -172,7 +163,6 @@ __device__ __forceinline__ void load_rows(const uint32_t* wq, uint32_t nq, uint3
     }
 }
 
-template <bool k16>
 __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint2* lq, uint32_t& nl, uint32_t* mq,
                                            uint32_t& nm, const uint16_t* __restrict__ prow,
                                            const uint16_t* __restrict__ plong, uint32_t* crow32, int lane) {
@@ -200,10 +190,10 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint32_t id = (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-            if (id < kMore) count<k16>(crow32, id);
+            if (id < kMore) count(crow32, id);
         }
-        if (nl > kLongCap - kWave) walk_long<k16>(lq, nl, plong, crow32, lane);
-        if (nm > kMidCap - kWave) walk_mid<k16>(mq, nm, prow, crow32, lane);
+        if (nl > kLongCap - kWave) walk_long(lq, nl, plong, crow32, lane);
+        if (nm > kMidCap - kWave) walk_mid(mq, nm, prow, crow32, lane);
         w = wn;
         r0 = n0;
         r1 = n1;
@@ -265,7 +255,6 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 
 // Phase 2 for one file: queue its narrow words (set bits of u64 words >= pb0) and walk their
 // postings into the wave's counter row.
-template <bool k16>
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0, uint32_t* wq,
                                               uint2* lq, uint32_t* mq, const uint16_t* __restrict__ prow,
                                               const uint16_t* __restrict__ plong, uint32_t* crow32, int lane,
@@ -293,7 +282,7 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
             const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
             if (total == 0) continue;
             if (nq + total > kWordCap) {
-                if (!(diag & 2)) walk_short<k16>(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
+                if (!(diag & 2)) walk_short(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
                 nq = 0;
             }
             if (total <= kWordCap) {
@@ -313,21 +302,21 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
                 if (has) wq[nq + lane_rank(bal)] = w;
                 nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
                 if (nq > kWordCap - kWave) {
-                    if (!(diag & 2)) walk_short<k16>(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
+                    if (!(diag & 2)) walk_short(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
                     nq = 0;
                 }
             }
         }
     }
-    if (!(diag & 2)) walk_short<k16>(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
-    walk_long<k16>(lq, nl, plong, crow32, lane);
-    walk_mid<k16>(mq, nm, prow, crow32, lane);
+    if (!(diag & 2)) walk_short(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
+    walk_long(lq, nl, plong, crow32, lane);
+    walk_mid(mq, nm, prow, crow32, lane);
 }
 
 // Phase 3 for one file: lanes = templates (t = lane + 64 j), overlap from the counter row
-// (u32 rows are re-zeroed for the wave's next file), the shared denominator and order; match
+// (re-zeroed for the wave's next file), the shared denominator and order; match
 // mode reduces over the wave, matrix mode writes the row and the top-k.
-template <bool kMatrix, int KM, bool k16, int TJ>
+template <bool kMatrix, int KM, int TJ>
 __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
                                            int32_t lf, bool cc, bool corpus_fast, double thr, int32_t* __restrict__ best_out,
                                            uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
@@ -343,13 +332,8 @@ __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, i
     for (int j = 0; j < TJ; ++j) {
         const int32_t t = lane + j * kWave;
         if (t < T) {
-            uint32_t ov;
-            if (k16) {
-                ov = reinterpret_cast<const uint16_t*>(crow32)[t];   // rows are rewritten per round
-            } else {
-                ov = crow32[t];
-                crow32[t] = 0;
-            }
+            const uint32_t ov = crow32[t];
+            crow32[t] = 0;
             const uint2 pc = tcs[t];   // {len | cc << 31, base | slack << 16}
             const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
                                      (int32_t)(pc.x >> 31));
@@ -448,7 +432,7 @@ __device__ __forceinline__ void post_narrow_body(
         const uint32_t wf = wfp[file];
         const int32_t lf = lenp[file];
         const bool cc = ccp[file] != 0;
-        file_postings<false>(row, w64, pb0, wq[wave], lq[wave], mq[wave], prow, plong, crow32, lane, diag);
+        file_postings(row, w64, pb0, wq[wave], lq[wave], mq[wave], prow, plong, crow32, lane, diag);
 
         if (diag & 8) {
 #pragma unroll
@@ -456,7 +440,7 @@ __device__ __forceinline__ void post_narrow_body(
                 if (lane + j * kWave < T) crow32[lane + j * kWave] = 0;
             continue;
         }
-        score_file<kMatrix, KM, false, kTJ>(crow32, tcs, T, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
+        score_file<kMatrix, KM, kTJ>(crow32, tcs, T, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
                                             k, mov, msc, tki, tks, lane);
     }
 }
@@ -484,115 +468,6 @@ __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
     post_narrow_body<true, KM>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, diag, false);
-}
-
-// ---- fused variant (DICE_POST_FUSED=1): no dense-partial matrix in HBM --------------------
-// One workgroup = 16 waves over 64 files in 4 rounds of 16; in round r wave w scores file
-// 16 r + w from u16 counter row w of buffer r & 1 (two buffers: the dense partials of round
-// r + 1 are computed while round r's files are walked). A dense job = 64 templates (lanes,
-// their masks in VGPRs) x the round's 16 files, whose first D words sit in LDS (staged by their
-// waves two rounds ahead: uniform ds_read_b64 broadcasts, in order, so they pipeline), written
-// straight into the counter rows. Waves take jobs from an LDS counter when their own file is
-// done, so the dense work fills the gaps between the waves' walks. One barrier per round.
-constexpr int kFusedMaxTpad = 608;   // LDS: 2 x 16 u16 rows + the staged words + the queues < 80 KiB
-
-template <int DP, int TPMAX>
-__device__ __forceinline__ void dense_jobs(uint32_t* jobctr, int64_t nf, int32_t T, const uint64_t* fws,
-                                           const uint64_t* __restrict__ dmask, uint16_t* buf, int lane) {
-    const int32_t ngroups = (T + kWave - 1) / kWave;
-    for (;;) {
-        uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(jobctr, 1u);
-        g = rfl(__shfl((int)g, 0));
-        if ((int32_t)g >= ngroups) break;
-        const int32_t t = (int32_t)g * kWave + lane;
-        const uint64_t* mp = dmask + (int64_t)(t < T ? t : 0) * kPostMaxDense;
-        // the prefix in passes of H words (H u64 masks = 2H VGPRs), partials summed in the row
-        constexpr int H = DP % 8 == 0 ? 8 : 4;
-        for (int h = 0; h < DP; h += H) {
-            uint32_t m[2 * H];
-#pragma unroll
-            for (int d = 0; d < H; ++d) {
-                const uint64_t v = t < T ? mp[h + d] : 0;   // zero past D (post_setup)
-                m[2 * d] = (uint32_t)v;
-                m[2 * d + 1] = (uint32_t)(v >> 32);
-            }
-            for (int f = 0; f < nf; ++f) {
-                const uint64_t* fw = fws + f * kPostMaxDense + h;
-                uint32_t acc[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int d = 0; d < H; ++d) {
-                    const uint64_t x = fw[d];   // uniform LDS address: broadcast
-                    acc[(2 * d) & 3] += __builtin_popcount((uint32_t)x & m[2 * d]);
-                    acc[(2 * d + 1) & 3] += __builtin_popcount((uint32_t)(x >> 32) & m[2 * d + 1]);
-                }
-                const uint32_t sum = acc[0] + acc[1] + acc[2] + acc[3];
-                if (t < T) buf[f * TPMAX + t] = (uint16_t)(h == 0 ? sum : buf[f * TPMAX + t] + sum);
-            }
-        }
-    }
-}
-
-template <int DP, int TPMAX>
-__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_fused_match(
-    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T,
-    const uint64_t* __restrict__ dmask, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-    const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
-    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
-    double* __restrict__ score_out, int32_t diag, bool corpus_fast) {
-    // diag as in post_narrow_body, plus 1: skip the dense jobs (results wrong)
-    constexpr int kRounds = kPostFiles / kPostWaves;
-    __shared__ uint32_t cnt32[2][kPostWaves * TPMAX / 2];        // u16 counters, [buffer][wave][TPMAX]
-    __shared__ uint64_t fws[2][kPostWaves * kPostMaxDense];      // staged dense words, [buffer][file][16]
-    __shared__ uint2 tcs[TPMAX];
-    __shared__ uint32_t wq[kPostWaves][kWordCap];
-    __shared__ uint2 lq[kPostWaves][kLongCap];
-    __shared__ uint32_t mq[kPostWaves][kMidCap];
-    __shared__ uint32_t jobs[kRounds];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = (int)rfl(threadIdx.x >> 6);
-    const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
-    const bool dense = D > 0 && !(diag & 1);
-    // files of round r: [f0 + 16 r, f0 + 16 r + nfr(r))
-    auto nfr = [&](int r) -> int64_t {
-        const int64_t a = f0 + (int64_t)r * kPostWaves;
-        return a >= n ? 0 : (n - a < kPostWaves ? n - a : kPostWaves);
-    };
-    // wave w stages its round-r file's first D words into fws[r & 1][w]
-    auto stage = [&](int r) {
-        const int64_t file = f0 + (int64_t)r * kPostWaves + wave;
-        if (file < n && lane < kPostMaxDense) fws[r & 1][wave * kPostMaxDense + lane] = lane < D ? rows[file * w64 + lane] : 0;
-    };
-    for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
-    if (threadIdx.x < kRounds) jobs[threadIdx.x] = 0;
-    if (!dense)   // no dense prefix: the rows start at zero every round
-        for (int i = threadIdx.x; i < 2 * kPostWaves * TPMAX / 2; i += kPostWaves * kWave) (&cnt32[0][0])[i] = 0;
-    stage(0);
-    stage(1);
-    __syncthreads();
-    if (dense) dense_jobs<DP, TPMAX>(&jobs[0], nfr(0), T, fws[0], dmask, reinterpret_cast<uint16_t*>(cnt32[0]), lane);
-    __syncthreads();
-    for (int r = 0; r < kRounds; ++r) {
-        uint32_t* crow32 = cnt32[r & 1] + wave * (TPMAX / 2);
-        const int64_t file = f0 + r * kPostWaves + wave;
-        if (file < n) {   // wave-uniform; every wave reaches the barrier below
-            file_postings<true>(rows + file * w64, w64, (diag & 4) ? w64 : D, wq[wave], lq[wave], mq[wave], prow, plong,
-                                crow32, lane, diag);
-            if (!(diag & 8))
-                score_file<false, 1, true, (TPMAX + kWave - 1) / kWave>(crow32, tcs, T, file, wfp[file], lenp[file],
-                                                                       ccp[file] != 0, corpus_fast, thr, best_out, ov_out,
-                                                                       score_out, 0, nullptr, nullptr, nullptr, nullptr,
-                                                                       lane);
-            if (!dense)   // re-zero for round r + 2
-                for (int i = lane; i < TPMAX / 2; i += kWave) crow32[i] = 0;
-        }
-        if (r + 1 < kRounds && dense)
-            dense_jobs<DP, TPMAX>(&jobs[r + 1], nfr(r + 1), T, fws[(r + 1) & 1], dmask,
-                                  reinterpret_cast<uint16_t*>(cnt32[(r + 1) & 1]), lane);
-        // round r + 2's words go to the buffer round r's jobs read (finished before the last barrier)
-        if (r + 2 < kRounds) stage(r + 2);
-        __syncthreads();
-    }
 }
 
 // ---- host side ---------------------------------------------------------------------------
@@ -696,8 +571,6 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
         hipMemcpy(c->d_ptc, tcv.data(), tcv.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "postings plan upload failed");
     c->post_dense = D;
-    const char* fu = getenv("DICE_POST_FUSED");
-    c->post_fused = fu && *fu && atoi(fu) != 0;
     const char* dg = getenv("DICE_POST_DIAG");
     c->post_diag = dg && *dg ? atoi(dg) : 0;
     c->post_tpad = tpad;
@@ -725,30 +598,8 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s) {
                        (const uint64_t*)c->d_pdm, (uint16_t*)b->d_pdense);
 }
 
-template <int DP, int TPMAX>
-static void launch_fused(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    const int64_t groups = (b->n + kPostFiles - 1) / kPostFiles;
-    hipLaunchKernelGGL((dice_post_fused_match<DP, TPMAX>), dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
-                       (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, (const uint64_t*)c->d_pdm,
-                       (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf, (const uint2*)c->d_ptc, b->d_wf,
-                       b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, c->post_diag, c->post_fast);
-}
-
-template <int TPMAX>
-static int launch_fused_dp(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    switch ((c->post_dense + 3) / 4) {
-        case 0:
-        case 1: launch_fused<4, TPMAX>(c, b, thr, s); break;
-        case 2: launch_fused<8, TPMAX>(c, b, thr, s); break;
-        case 3: launch_fused<12, TPMAX>(c, b, thr, s); break;
-        default: launch_fused<16, TPMAX>(c, b, thr, s); break;
-    }
-    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post_fused launch failed");
-}
-
 template <bool kMatrix, int KM>
 static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t s) {
-    if (!kMatrix && c->post_fused && c->post_tp <= kFusedMaxTpad) return launch_fused_dp<kFusedMaxTpad>(c, b, thr, s);
     const size_t need = (size_t)b->capacity * c->post_tp * 2;
     if (b->pdense_bytes < need) {
         if (b->d_pdense) (void)hipFree(b->d_pdense);
