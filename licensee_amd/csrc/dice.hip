@@ -38,14 +38,15 @@ std::string& last_error() {
 
 // Row-major uint64 bitsets [n][W64] -> tile layout [n_tiles][Wq][64] uint4 (zero padded).
 __global__ __launch_bounds__(256) void dice_pack_tiles(const uint64_t* __restrict__ rows, int64_t n,
-                                                       int32_t w64, int32_t wq,
+                                                       int32_t w64, int32_t wq, const int32_t* __restrict__ qperm,
                                                        uint4* __restrict__ tiles, int64_t n_tiles) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = n_tiles * wq * kWave;
     if (gid >= total) return;
     const int lane = (int)(gid & (kWave - 1));
     const int64_t tq = gid >> 6;
-    const int q = (int)(tq % wq);
+    const int slot = (int)(tq % wq);
+    const int q = qperm ? qperm[slot] : slot;   // tile slot -> vocabulary quad (sparse program order)
     const int64_t tile = tq / wq;
     const int64_t file = tile * kWave + lane;
     uint64_t a = 0, b = 0;
@@ -282,6 +283,7 @@ static void ctx_free(dice_ctx* c) {
     if (c->scratch) dice_batch_destroy(c->scratch);
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
+    if (c->d_qperm) (void)hipFree(c->d_qperm);
     void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc};
     for (void* p : plan)
         if (p) (void)hipFree(p);
@@ -442,7 +444,7 @@ int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
     const int64_t total = n_tiles * c->wq * kWave;
     const unsigned grid = (unsigned)((total + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(dice_pack_tiles, dim3(grid), dim3(kBlock), 0, s, b->d_rows, n, c->w64, c->wq,
-                       b->d_tiles, n_tiles);
+                       c->kind == 1 ? (const int32_t*)c->d_qperm : nullptr, b->d_tiles, n_tiles);
     HIP_TRY(hipGetLastError());
     return DICE_OK;
 }

@@ -43,6 +43,7 @@ struct dice_ctx {
     hipFunction_t prog_match = nullptr;
     hipFunction_t prog_matrix = nullptr;    // top-k <= 4
     hipFunction_t prog_matrix16 = nullptr;  // top-k <= 16
+    int32_t* d_qperm = nullptr;             // sparse program tile slot -> vocabulary quad (kind 1)
     dice_batch* scratch = nullptr;  // reused by the host-buffer calls
     // kind 2 plan (dice_lds.hip): per-(slab, template) entry runs, entries, wave split
     void* d_lrec = nullptr;

@@ -116,15 +116,18 @@ __device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
 )HIP";
 
 const char* kMatchKernel = R"HIP(
-extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
+extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_match(
     const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
     const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
     u32* __restrict__ ov_out, double* __restrict__ score_out) {
     const int lane = threadIdx.x & 63;
-    const i64 tile = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const i64 tile = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (tile * 64 >= n) return;
     const i64 file = tile * 64 + lane;
     const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
+#if WAVE_TIMING
+    const u64 t0_ = __builtin_amdgcn_s_memrealtime();
+#endif
     const u32 wf = wfp[file];
     const i32 lf = lenp[file];
     const bool cc = ccp[file] != 0;
@@ -145,17 +148,28 @@ extern "C" __global__ __launch_bounds__(256 MATCH_WAVES) void dice_prog_match(
         MSTORE(ov_out + file, bov);
         MSTORE(score_out + file, s);
     }
+#if WAVE_TIMING
+    // diagnostics (DICE_PROG_DIAG=timing, results wrong): per wave its start and end real-time (100 MHz)
+    // clock and the raw HW_ID / XCC_ID registers, in the tile's first output slots
+    const u64 t1_ = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        score_out[tile * 64] = (double)t0_;
+        score_out[tile * 64 + 1] = (double)t1_;
+        ov_out[tile * 64] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        ov_out[tile * 64 + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+#endif
 }
 )HIP";
 
 // Matrix kernel template: KM is the compile-time top-k slot count (4 or 16).
 const char* kMatrixKernel = R"HIP(
-extern "C" __global__ __launch_bounds__(256) void KNAME(
+extern "C" __global__ __launch_bounds__(64 * WPB) void KNAME(
     const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
     const unsigned char* __restrict__ ccp, i32 k, u32* __restrict__ ov_out, double* __restrict__ score_out,
     i32* __restrict__ topk_idx, double* __restrict__ topk_score) {
     const int lane = threadIdx.x & 63;
-    const i64 tile = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const i64 tile = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (tile * 64 >= n) return;
     const i64 file = tile * 64 + lane;
     const bool valid = file < n;
@@ -354,8 +368,9 @@ static void emit_macro(std::ostringstream& s, const std::string& head, const std
 //       epilogue (denominator, compare) runs once per template after the last quad.
 //   't' template-major: the whole file bitset is loaded up front (WQ*4 VGPRs) and each
 //       template is accumulated and retired in turn.
-std::string program_source(const dice_templates* t, const Program& p, int32_t wq, bool corpus_fast) {
+std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool corpus_fast) {
     std::ostringstream s;
+    s << "#define WPB " << p.wpb << "\n";
     const char* waves = getenv("DICE_PROG_WAVES");  // optional occupancy floor (waves/SIMD) for A/B runs
     const char* order_env = getenv("DICE_PROG_ORDER");
     const char order = (order_env && *order_env == 't') ? 't' : 'd';
@@ -477,6 +492,26 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
             quads.swap(q2);
             range.swap(r2);
         }
+        // Tile layout in processing order (DICE_PROG_QLAYOUT=vocab keeps vocabulary order): tile
+        // slot i holds the vocabulary quad processed i-th (dice_pack_tiles applies p.qperm), so a
+        // wave's loads walk its 28 KiB tile front to back while the VALU work stays zipped.
+        {
+            const char* ql = getenv("DICE_PROG_QLAYOUT");
+            p.qperm.clear();
+            if (!(ql && strcmp(ql, "vocab") == 0)) {
+                std::vector<char> seen((size_t)wq, 0);
+                for (int32_t q : quads) {
+                    p.qperm.push_back(q);
+                    seen[(size_t)q] = 1;
+                }
+                for (int32_t q = 0; q < wq; ++q)
+                    if (!seen[(size_t)q]) p.qperm.push_back(q);   // quads no template reads (never loaded)
+                for (size_t i = 0; i < quads.size(); ++i) quads[i] = (int32_t)i;
+            }
+            s << "// QPERM";
+            for (int32_t q : p.qperm) s << " " << q;
+            s << "\n";
+        }
         const char* sched_env = getenv("DICE_PROG_SCHED");
         const bool ring = sched_env && strcmp(sched_env, "ring") == 0;
         if (ring) {
@@ -537,6 +572,7 @@ std::string program_source(const dice_templates* t, const Program& p, int32_t wq
     }
     emit_macro(s, "FILE_PROLOGUE", prologue.str());
     const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
+    s << "#define WAVE_TIMING " << (diag && strcmp(diag, "timing") == 0 ? 1 : 0) << "\n";
     if (diag && strcmp(diag, "noepi") == 0) {
         std::ostringstream mb;
         mb << "bd = 1; bo = 0; _Pragma(\"unroll\") for (int i = 0; i < NT; ++i) bo += acc[i];\n";
@@ -617,6 +653,8 @@ static bool corpus_in_fast_envelope(const dice_templates* t) {
 static std::string source_for(const dice_templates* t, Program& prog) {
     const int32_t w64 = (t->n_vocab + 63) / 64;
     build_entries(t, w64, prog);
+    const char* wpb = getenv("DICE_PROG_WPB");   // waves per workgroup (A/B runs; default 4)
+    prog.wpb = wpb && *wpb ? std::max(1, std::min(16, atoi(wpb))) : 4;
     return program_source(t, prog, (w64 + 1) / 2, corpus_in_fast_envelope(t));
 }
 
@@ -631,31 +669,40 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
     const std::string src = source_for(t, c->prog);
     int rc = compile_or_load(c, src);
     if (rc != DICE_OK) return rc;
+    if (!c->prog.qperm.empty()) {
+        const size_t bytes = c->prog.qperm.size() * sizeof(int32_t);
+        if (c->prog.qperm.size() != (size_t)c->wq) return fail(DICE_E_STATE, "program tile permutation size");
+        if ((rc = dalloc_bytes(reinterpret_cast<void**>(&c->d_qperm), bytes)) != DICE_OK) return rc;
+        if (hipMemcpy(c->d_qperm, c->prog.qperm.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(DICE_E_DEVICE, "program tile permutation upload failed");
+    }
     c->kind = 1;
     return DICE_OK;
 }
 
 int program_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + 63) / 64;
-    const unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    const int32_t wpb = c->prog.wpb;
+    const unsigned grid = (unsigned)((n_tiles + wpb - 1) / wpb);
     hipFunction_t fn = c->prog_match;
     int64_t n = b->n;
     void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score};
-    if (hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+    if (hipModuleLaunchKernel(fn, grid, 1, 1, 64 * wpb, 1, 1, 0, s, args, nullptr) != hipSuccess)
         return fail(DICE_E_DEVICE, "launch dice_prog_match failed");
     return DICE_OK;
 }
 
 int program_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s) {
     const int64_t n_tiles = (b->n + 63) / 64;
-    const unsigned grid = (unsigned)((n_tiles + 3) / 4);
+    const int32_t wpb = c->prog.wpb;
+    const unsigned grid = (unsigned)((n_tiles + wpb - 1) / wpb);
     int64_t n = b->n;
     int32_t kk = k;
     int32_t* tki = k > 0 ? b->d_tki : nullptr;
     double* tks = k > 0 ? b->d_tks : nullptr;
     void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &kk, &b->d_mov, &b->d_mscore, &tki, &tks};
     hipFunction_t fn = k <= 4 ? c->prog_matrix : c->prog_matrix16;
-    if (hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+    if (hipModuleLaunchKernel(fn, grid, 1, 1, 64 * wpb, 1, 1, 0, s, args, nullptr) != hipSuccess)
         return fail(DICE_E_DEVICE, "launch dice_prog_matrix failed");
     return DICE_OK;
 }

@@ -21,6 +21,8 @@ struct Entry {
 struct Program {
     std::vector<Entry> prog;          // sorted by (dword, tpl)
     std::vector<int32_t> dword_map;   // vocab dword -> file dword in the remapped layout (-1: unused)
+    int32_t wpb = 4;                  // waves (64-file tiles) per workgroup
+    std::vector<int32_t> qperm;       // tile slot -> vocabulary quad (empty: identity)
     size_t entries() const { return prog.size(); }
 };
 

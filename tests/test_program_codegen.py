@@ -18,13 +18,26 @@ from tests.helpers import NormFile, make_files
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def tile_pack(bits: np.ndarray, wq: int) -> np.ndarray:
-    """Row-major [n][w64] uint64 -> tile layout [n_tiles][wq][64] of 4 x uint32."""
+def tile_pack(bits: np.ndarray, wq: int, qperm=None) -> np.ndarray:
+    """Row-major [n][w64] uint64 -> tile layout [n_tiles][wq][64] of 4 x uint32; with ``qperm``
+    tile slot i holds vocabulary quad qperm[i] (dice_pack_tiles)."""
     n, w64 = bits.shape
     nt = (n + 63) // 64
     d32 = np.zeros((nt * 64, wq * 4), np.uint32)
     d32[:n, :w64 * 2] = bits.view(np.uint32).reshape(n, w64 * 2)
-    return np.ascontiguousarray(d32.reshape(nt, 64, wq, 4).transpose(0, 2, 1, 3))
+    t = d32.reshape(nt, 64, wq, 4)
+    if qperm is not None:
+        t = t[:, :, np.asarray(qperm, np.int64), :]
+    return np.ascontiguousarray(t.transpose(0, 2, 1, 3))
+
+
+def source_qperm(src: str):
+    """The tile permutation a generated program declares (`// QPERM ...`), or None (identity)."""
+    for line in src.splitlines():
+        if line.startswith('// QPERM'):
+            q = [int(x) for x in line.split()[2:]]
+            return q or None
+    return None
 
 
 def _templates_struct(corpus):
@@ -58,7 +71,9 @@ def run_host(corpus, fb, k, tmp_path, with_votes=False):
     wq = (corpus.w64 + 1) // 2
     n = fb.n
     npad = ((n + 63) // 64) * 64
-    tile_pack(fb.bits, wq).tofile(os.path.join(d, 'tiles.bin'))
+    qperm = source_qperm(src)
+    assert qperm is None or sorted(qperm) == list(range(wq))
+    tile_pack(fb.bits, wq, qperm).tofile(os.path.join(d, 'tiles.bin'))
     for name, arr, dt in (('wf', fb.wordset_size, np.uint32), ('len', fb.length, np.int32),
                           ('cc', fb.cc_false_positive, np.uint8)):
         pad = np.zeros(npad, dt)
