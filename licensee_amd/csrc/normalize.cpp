@@ -177,12 +177,9 @@ constexpr struct ByteMasks {
 } kByteMasks;
 
 inline uint64_t key_mix(uint64_t lo, uint64_t hi, uint64_t len, uint64_t tail) {
-    uint64_t h = lo ^ (hi * 0xC2B2AE3D27D4EB4FULL) ^ (len << 56) ^ tail;
-    h ^= h >> 33;   // fmix64: every output bit depends on every input bit (slots are low bits)
-    h *= 0xFF51AFD7ED558CCDULL;
-    h ^= h >> 33;
-    h *= 0xC4CEB9FE1A85EC53ULL;
-    return h ^ (h >> 33);
+    // one multiply; its high half (well mixed) folded into the low bits the tables index by
+    const uint64_t p = (lo ^ (hi * 0xC2B2AE3D27D4EB4FULL) ^ (len << 56) ^ tail) * 0x9E3779B97F4A7C15ULL;
+    return p ^ (p >> 32);
 }
 
 template <class C>
@@ -241,51 +238,78 @@ inline bool tail_equal(const std::string& w, const char32_t* p) {
     return true;
 }
 
-// The template vocabulary: open addressing over 32-bit slots (id + 1 in the low id_bits, a
-// hash tag above; 0 = empty) small enough to stay in L1, the packed keys in id order for the
-// compare; words kept for the tail compare of long words.
+// The template vocabulary: buckets of 8 32-bit slots (id + 1 in the low id_bits, a hash tag
+// above; 0 = empty), 32 KiB at the vendored corpus's 3.5k words so it stays in L1; a lookup
+// compares a whole bucket's tags in one vector compare (almost every token is a hit, so there
+// is no probe loop to mispredict), then the packed key of the one candidate (keys in id order);
+// words kept for the tail compare of long words. A full bucket overflows into the next one.
 struct VocabTable {
     struct Key {
         uint64_t lo, hi;
         uint32_t len;
     };
-    std::vector<uint32_t> slot;
+    static constexpr size_t kBucket = 8;
+    std::vector<uint32_t> slot;   // [n_buckets][8], 32-byte aligned rows (see build)
     std::vector<Key> key;
     std::vector<std::string> words;
-    uint64_t mask = 0;
+    size_t bmask = 0, base = 0;   // buckets - 1; first aligned slot in `slot`
     int id_bits = 1;
     uint32_t id_mask = 1;
     uint32_t tag(uint64_t h) const { return (uint32_t)(h >> 40) << id_bits; }
+    const uint32_t* bucket(size_t b) const { return slot.data() + base + b * kBucket; }
     void build(int32_t n, const char* const* vocab) {
-        size_t cap = 16;
-        while (cap < 2 * (size_t)n + 1) cap <<= 1;
+        size_t nb = 2;
+        while (nb * kBucket < 2 * (size_t)n + 1) nb <<= 1;
         id_bits = 1;
         while (((uint64_t)1 << id_bits) <= (uint64_t)n + 1) ++id_bits;
         if (id_bits > 28) throw std::runtime_error("vocabulary too large for the host word table");
         id_mask = (1u << id_bits) - 1;
-        slot.assign(cap, 0);
+        slot.assign(nb * kBucket + kBucket, 0);
+        base = (size_t)((32 - ((uintptr_t)slot.data() & 31)) & 31) / sizeof(uint32_t);
+        bmask = nb - 1;
         key.resize((size_t)n);
-        mask = cap - 1;
         words.assign(vocab, vocab + n);
         for (int32_t i = 0; i < n; ++i) {
             const WordKey k = word_key(words[i]);
             key[(size_t)i] = Key{k.lo, k.hi, k.len};
-            size_t j = k.h & mask;
-            while (slot[j]) j = (j + 1) & mask;
-            slot[j] = tag(k.h) | (uint32_t)(i + 1);
+            for (size_t b = k.h & bmask;; b = (b + 1) & bmask) {
+                uint32_t* r = slot.data() + base + b * kBucket;
+                size_t j = 0;
+                while (j < kBucket && r[j]) ++j;
+                if (j < kBucket) {
+                    r[j] = tag(k.h) | (uint32_t)(i + 1);
+                    break;
+                }
+            }
         }
     }
     int32_t find(const WordKey& k, const char32_t* p) const {
-        if (slot.empty()) return -1;
+        if (key.empty()) return -1;
         const uint32_t t = tag(k.h);
-        for (size_t j = k.h & mask;; j = (j + 1) & mask) {
-            const uint32_t s = slot[j];
-            if (!s) return -1;
-            if ((s & ~id_mask) != t) continue;
-            const int32_t id = (int32_t)(s & id_mask) - 1;
-            const Key& e = key[(size_t)id];
-            if (e.lo == k.lo && e.hi == k.hi && e.len == k.len && (k.len <= 16 || tail_equal(words[(size_t)id], p)))
-                return id;
+        for (size_t b = k.h & bmask;; b = (b + 1) & bmask) {
+            const uint32_t* r = bucket(b);
+            uint32_t hit, empty;
+#if defined(__AVX2__)
+            const __m256i v = _mm256_loadu_si256((const __m256i*)r);   // aligned when the table was built in place
+            hit = scan::lanes(_mm256_cmpeq_epi32(_mm256_and_si256(v, _mm256_set1_epi32((int)~id_mask)),
+                                                 _mm256_set1_epi32((int)t)));
+            empty = scan::lanes(_mm256_cmpeq_epi32(v, _mm256_setzero_si256()));
+#else
+            hit = empty = 0;
+            for (size_t j = 0; j < kBucket; ++j) {
+                hit |= (uint32_t)(r[j] && (r[j] & ~id_mask) == t) << j;
+                empty |= (uint32_t)(r[j] == 0) << j;
+            }
+#endif
+            hit &= ~empty;
+            while (hit) {
+                const int32_t id = (int32_t)(r[__builtin_ctz(hit)] & id_mask) - 1;
+                const Key& e = key[(size_t)id];
+                if (e.lo == k.lo && e.hi == k.hi && e.len == k.len && (k.len <= 16 || tail_equal(words[(size_t)id], p)))
+                    return id;
+                hit &= hit - 1;
+            }
+            if (empty) return -1;
         }
     }
 };
