@@ -42,6 +42,9 @@
 
 namespace dice {
 
+#ifndef DENSE_TU
+#define DENSE_TU 2
+#endif
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
@@ -229,17 +232,33 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
         // template masks: wave-uniform scalar loads (scalar returns are unordered, so a prefetch
         // would be waited for with the current template's masks: no software pipelining; the
         // other waves of the SIMD cover the latency)
-        for (int32_t t = tb; t < te; ++t) {
-            const uint64_t* m = dmask + (int64_t)t * kPostMaxDense;
-            // four independent accumulator chains (a single v_bcnt chain stalls on its latency)
-            uint32_t acc[4] = {0, 0, 0, 0};
+        // TU = 2 templates per iteration, word-major, so both templates' mask loads are in flight
+        // before the first wait (1 -> 2: config 3 5.39 -> 5.26 ms)
+        constexpr int TU = DENSE_TU;
+        for (int32_t t0 = tb; t0 < te; t0 += TU) {
+            uint32_t acc[TU][4];
+            const uint64_t* m[TU];
 #pragma unroll
-            for (int d = 0; d < DP; ++d) {
-                const uint64_t md = m[d];
-                acc[(2 * d) & 3] += __builtin_popcount((uint32_t)fd[d] & (uint32_t)md);
-                acc[(2 * d + 1) & 3] += __builtin_popcount((uint32_t)(fd[d] >> 32) & (uint32_t)(md >> 32));
+            for (int u = 0; u < TU; ++u) {
+                // the last iteration of an odd range repeats template te - 1 (same value)
+                m[u] = dmask + (int64_t)(t0 + u < te ? t0 + u : te - 1) * kPostMaxDense;
+                // four independent accumulator chains (a single v_bcnt chain stalls on its latency)
+                acc[u][0] = acc[u][1] = acc[u][2] = acc[u][3] = 0;
             }
-            crow[t] = (uint16_t)(acc[0] + acc[1] + acc[2] + acc[3]);
+            // word-major over the TU templates: every template's masks are live together
+#pragma unroll
+            for (int d = 0; d < DP; ++d)
+#pragma unroll
+                for (int u = 0; u < TU; ++u) {
+                    const uint64_t md = m[u][d];
+                    acc[u][(2 * d) & 3] += __builtin_popcount((uint32_t)fd[d] & (uint32_t)md);
+                    acc[u][(2 * d + 1) & 3] += __builtin_popcount((uint32_t)(fd[d] >> 32) & (uint32_t)(md >> 32));
+                }
+#pragma unroll
+            for (int u = 0; u < TU; ++u) {
+                const int32_t t = t0 + u < te ? t0 + u : te - 1;
+                crow[t] = (uint16_t)(acc[u][0] + acc[u][1] + acc[u][2] + acc[u][3]);
+            }
         }
         for (int32_t t = T + (threadIdx.x >> 6); t < tp; t += kPostWaves) crow[t] = 0;   // row padding
     }
