@@ -185,16 +185,22 @@ def parity_sample(run, orc, sptr, threads, n_sample):
     sl = slice(0, min(n_sample, run.n_per))
     if run.cfg != 5:
         best, ov, score = run.batch.download_match(sptr)
+        t0 = time.perf_counter()
         eb, eo, es = orc.match(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl],
                                run.args.threshold, nthreads=threads, mode=0)
+        cpu_s = time.perf_counter() - t0
         mism = int(np.sum(best[sl] != eb) + np.sum(ov[sl] != eo) + np.sum(score[sl] != es))
-        return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
+        return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)',
+                'oracle_files_per_s': sl.stop / cpu_s}
     ovm, scm, tki, tks = run.batch.download_matrix(run.args.topk, sptr)
+    t0 = time.perf_counter()
     mov, msc = orc.matrix(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl], nthreads=threads)
+    cpu_s = time.perf_counter() - t0
     mism = int(np.sum(ovm[sl] != mov) + np.sum(scm[sl] != msc))
     rows = np.arange(sl.stop)
     mism += int(np.sum(scm[rows, tki[sl, 0]] != tks[sl, 0]))
-    return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (matrix, hash Set#&)'}
+    return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (matrix, hash Set#&)',
+            'oracle_files_per_s': sl.stop / cpu_s}
 
 
 def main():
@@ -337,6 +343,7 @@ def main():
             parity = {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
         else:
             parity = parity_sample(run, orc, sptr, cpu_threads, sample)
+            parity.pop('oracle_files_per_s', None)
 
     head = {'templates': run.T, 'vocab': run.V, 'kernel': KERNELS[run.kind], 'program_entries': run.entries,
             'algorithmic_bytes_per_file': run.algo_bytes_per_file}
@@ -360,6 +367,11 @@ def main():
             if not args.no_cpu_baseline:
                 rec['parity'] = parity_sample(r, oracle_for(r.corpus), sptr, cpu['threads'],
                                               {3: 20_000, 4: 30_000, 5: 50_000}[c])
+                # the parity leg is the reference-equivalent CPU path on the same files: its rate
+                rec['cpu_baseline'] = {'value': rec['parity'].pop('oracle_files_per_s'), 'unit': 'files/s',
+                                       'cores': cpu['threads'], 'kind': 'port',
+                                       'sample': f"the parity sample: first {rec['parity']['checked_files']} files, "
+                                                 f"hash-set Set#& restatement (oracle/dice_ref.c)"}
             extras['configs'][str(c)] = rec
             log(f"config {c}: {rec['files_per_s']:.3e} files/s, launch {lm * 1e3:.1f} us, "
                 f"frac {rec['roofline_frac']:.3f}, parity {rec.get('parity')}")
