@@ -45,6 +45,9 @@ namespace dice {
 #ifndef DENSE_TU
 #define DENSE_TU 2
 #endif
+#ifndef POST_PREFETCH_WORDS
+#define POST_PREFETCH_WORDS 0   // 1: prefetch_file also loads the first word chunks (spills at 64 VGPRs)
+#endif
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
@@ -274,10 +277,10 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 
 // Phase 2 for one file: queue its narrow words (set bits of u64 words >= pb0) and walk their
 // postings into the wave's counter row.
-__device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0, uint32_t* wq,
-                                              uint2* lq, uint32_t* mq, const uint16_t* __restrict__ prow,
-                                              const uint16_t* __restrict__ plong, uint32_t* crow32, int lane,
-                                              int32_t diag) {
+__device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
+                                              const uint64_t (&first)[kChunks], uint32_t* wq, uint2* lq, uint32_t* mq,
+                                              const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+                                              uint32_t* crow32, int lane, int32_t diag) {
     uint32_t nq = 0;           // queued narrow words (wave-uniform)
     uint32_t nl = 0, nm = 0;   // queued long / mid words (uniform)
 
@@ -290,7 +293,7 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) {
             const int32_t p = pb + c * kWave + lane;
-            xs[c] = p < w64 ? row[p] : 0;
+            xs[c] = (POST_PREFETCH_WORDS && pb == pb0) ? first[c] : (p < w64 ? row[p] : 0);
         }
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) {
@@ -401,6 +404,41 @@ __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, i
     }
 }
 
+// A file's loads that do not depend on its walk -- dense partials, scalars, first word chunks --
+// issued while the wave is still scoring the previous file (prefetch_file), so they are in
+// flight during that file's scoring instead of heading this file's dependency chain.
+constexpr int kPJ = (kPostMaxTpad / 2 + kWave - 1) / kWave;   // u32 partial pairs per lane
+
+struct FilePre {
+    uint32_t part[kPJ];
+    uint64_t first[kChunks];
+    uint32_t wf, cc;
+    int32_t lf;
+};
+
+__device__ __forceinline__ void prefetch_file(int64_t file, const uint64_t* __restrict__ rows, int32_t w64,
+                                              int32_t pb0, const uint16_t* __restrict__ dense, int32_t tp,
+                                              const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+                                              const uint8_t* __restrict__ ccp, int lane, FilePre& p) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + file * tp);
+#pragma unroll
+    for (int j = 0; j < kPJ; ++j) {
+        const int32_t i = lane + j * kWave;
+        p.part[j] = i < tp / 2 ? src[i] : 0;
+    }
+    if (POST_PREFETCH_WORDS) {
+        const uint64_t* row = rows + file * w64;
+#pragma unroll
+        for (int c = 0; c < kChunks; ++c) {
+            const int32_t q = pb0 + c * kWave + lane;
+            p.first[c] = q < w64 ? row[q] : 0;
+        }
+    }
+    p.wf = wfp[file];
+    p.lf = lenp[file];
+    p.cc = ccp[file];
+}
+
 // Phases 2 + 3, one file per wave (16 waves x 4 files per workgroup). Each wave owns one u32
 // counter row in LDS (zero between files). Narrow words are queued from the file's u64 words
 // >= D and walked (walk_short / walk_mid / walk_long) after the file's dense partials (from
@@ -431,27 +469,29 @@ __device__ __forceinline__ void post_narrow_body(
     __syncthreads();
 
     const int32_t pb0 = (diag & 4) ? w64 : D;
+    FilePre pre;
+    if (f0 + wave < n) prefetch_file(f0 + wave, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
         const int64_t file = f0 + fi;
         if (file >= n) break;   // wave-uniform
         const uint64_t* row = rows + file * w64;
         // this file's dense partials start its counter row (a plain copy, u16 pairs widened: the
         // row is zero here and this wave's postings adds come after it)
-        {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + file * tp);
 #pragma unroll
-            for (int j = 0; j < (kPostMaxTpad / 2 + kWave - 1) / kWave; ++j) {
-                const int32_t i = lane + j * kWave;
-                if (i < tp / 2) {
-                    const uint32_t v = src[i];
-                    *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(v & 0xFFFFu, v >> 16);
-                }
-            }
+        for (int j = 0; j < kPJ; ++j) {
+            const int32_t i = lane + j * kWave;
+            if (i < tp / 2) *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
         }
-        const uint32_t wf = wfp[file];
-        const int32_t lf = lenp[file];
-        const bool cc = ccp[file] != 0;
-        file_postings(row, w64, pb0, wq[wave], lq[wave], mq[wave], prow, plong, crow32, lane, diag);
+        const uint32_t wf = pre.wf;
+        const int32_t lf = pre.lf;
+        const bool cc = pre.cc != 0;
+        uint64_t first[kChunks];
+#pragma unroll
+        for (int c = 0; c < kChunks; ++c) first[c] = POST_PREFETCH_WORDS ? pre.first[c] : 0;
+        file_postings(row, w64, pb0, first, wq[wave], lq[wave], mq[wave], prow, plong, crow32, lane, diag);
+        // the wave's next file: its independent loads fly while this one is scored
+        if (fi + kPostWaves < kPostFiles && file + kPostWaves < n)
+            prefetch_file(file + kPostWaves, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
 
         if (diag & 8) {
 #pragma unroll
