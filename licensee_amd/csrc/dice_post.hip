@@ -24,8 +24,8 @@
 //            LDS list, slots assigned by a DPP wave prefix sum; walk_short gives each queued
 //            word one lane, reads its 32-byte postings row (16 entries, each a byte offset
 //            4*t into the counter row, 0xFFFF padding) and adds 1 to the first 8 listed
-//            counters (ds_add_u32); words with 9-16 entries wait in a mid queue (entries 8-15),
-//            longer ones in a long queue walked by all 64 lanes from the plong array. Scoring
+//            counters (ds_add_u32), words with 9-16 entries their other 8 too; longer ones
+//            wait in a long queue walked by all 64 lanes from the plong array. Scoring
 //            reads (and re-zeroes) the row with lanes = templates (t = lane + 64 j), using the
 //            packed template constants {len | cc << 31, base | slack << 16}: the same
 //            denominator, IEEE score and strict order (score, then later key) as every other
@@ -53,8 +53,7 @@ constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
 constexpr int kPostMaxDense = 16;        // dense prefix u64 words (20 / 24 measured slower at T = 600)
 constexpr int kRowW = 16;                // template ids per postings row
-constexpr int kWordCap = 192;            // per-wave queue of narrow word ids
-constexpr int kMidCap = 128;             // per-wave queue of words with 9-16 postings
+constexpr int kWordCap = 320;            // per-wave queue of narrow word ids
 constexpr uint16_t kNoTpl = 0xFFFF;      // empty row entry
 constexpr uint16_t kMore = 0xFFFE;       // row entry 15: a long word (entries 0-1 offset, 2 length)
 constexpr int kLongCap = 64;             // per-wave queue of long words (offset, length)
@@ -134,27 +133,10 @@ __device__ __forceinline__ void walk_long(const uint2* lq, uint32_t& nl, const u
     nl = 0;
 }
 
-// Second halves (entries 8-15) of the queued MID words (9-16 postings), one lane per word.
-__device__ __forceinline__ void walk_mid(const uint32_t* mq, uint32_t& nm, const uint16_t* __restrict__ prow,
-                                         uint32_t* crow32, int lane) {
-    for (uint32_t e0 = 0; e0 < nm; e0 += kWave) {
-        const uint32_t e = e0 + lane;
-        uint4 r1 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (e < nm) r1 = reinterpret_cast<const uint4*>(prow + (int64_t)mq[e] * kRowW)[1];
-        const uint32_t rr[4] = {r1.x, r1.y, r1.z, r1.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t id = (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-            if (id < kMore) count(crow32, id);
-        }
-    }
-    nm = 0;
-}
-
 // Queued narrow words, one lane per word: its 32-byte row in two loads, then the first 8
-// template ids (8 predicated counter adds). Words with more ids wait in the mid queue (ids
-// 8-15) or, past 16, in the long queue; each queue is walked once it holds >= 64 words, so
-// its passes run with (nearly) every lane busy.
+// template ids (8 predicated counter adds) and, for words with 9-16 ids, the row's other 8
+// right away (their half is already loaded: no second pass). Words past 16 ids wait in the
+// long queue, walked once it holds >= 64 words so its passes run with (nearly) every lane busy.
 __device__ __forceinline__ void load_rows(const uint32_t* wq, uint32_t nq, uint32_t e0, const uint16_t* __restrict__ prow,
                                           int lane, uint32_t& w, uint4& r0, uint4& r1) {
     const uint32_t e = e0 + lane;
@@ -169,8 +151,8 @@ __device__ __forceinline__ void load_rows(const uint32_t* wq, uint32_t nq, uint3
     }
 }
 
-__device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint2* lq, uint32_t& nl, uint32_t* mq,
-                                           uint32_t& nm, const uint16_t* __restrict__ prow,
+__device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint2* lq, uint32_t& nl,
+                                           const uint16_t* __restrict__ prow,
                                            const uint16_t* __restrict__ plong, uint32_t* crow32, int lane) {
     uint32_t w;
     uint4 r0, r1;
@@ -182,15 +164,11 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
         if (e0 + kWave < nq) load_rows(wq, nq, e0 + kWave, prow, lane, wn, n0, n1);
         const bool lng = (r1.w >> 16) == kMore;
         const bool mid = !lng && (r1.x & 0xFFFFu) != kNoTpl;
-        const uint64_t bl = __ballot(lng), bm = __ballot(mid);
+        const uint64_t bl = __ballot(lng);
         if (bl) {
             if (lng) lq[nl + lane_rank(bl)] = make_uint2(r0.x, r0.y & 0xFFFFu);   // (offset, length)
             nl = rfl(nl + (uint32_t)__builtin_popcountll(bl));
             if (lng) r0 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        }
-        if (bm) {
-            if (mid) mq[nm + lane_rank(bm)] = w;
-            nm = rfl(nm + (uint32_t)__builtin_popcountll(bm));
         }
         const uint32_t rr[4] = {r0.x, r0.y, r0.z, r0.w};
 #pragma unroll
@@ -198,8 +176,15 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
             const uint32_t id = (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
             if (id < kMore) count(crow32, id);
         }
+        if (__ballot(mid)) {   // words with 9-16 ids: entries 8-15 from the row's loaded second half
+            const uint32_t r2[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t id = (r2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+                if (mid && id < kMore) count(crow32, id);
+            }
+        }
         if (nl > kLongCap - kWave) walk_long(lq, nl, plong, crow32, lane);
-        if (nm > kMidCap - kWave) walk_mid(mq, nm, prow, crow32, lane);
         w = wn;
         r0 = n0;
         r1 = n1;
@@ -278,11 +263,11 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // Phase 2 for one file: queue its narrow words (set bits of u64 words >= pb0) and walk their
 // postings into the wave's counter row.
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
-                                              const uint64_t (&first)[kChunks], uint32_t* wq, uint2* lq, uint32_t* mq,
+                                              const uint64_t (&first)[kChunks], uint32_t* wq, uint2* lq,
                                               const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
                                               uint32_t* crow32, int lane, int32_t diag) {
     uint32_t nq = 0;           // queued narrow words (wave-uniform)
-    uint32_t nl = 0, nm = 0;   // queued long / mid words (uniform)
+    uint32_t nl = 0;           // queued long words (uniform)
 
     // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
     // together. Per chunk a wave prefix sum of the lanes' bit counts gives every lane its
@@ -304,7 +289,7 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
             const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
             if (total == 0) continue;
             if (nq + total > kWordCap) {
-                if (!(diag & 2)) walk_short(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
+                if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
                 nq = 0;
             }
             if (total <= kWordCap) {
@@ -324,15 +309,14 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
                 if (has) wq[nq + lane_rank(bal)] = w;
                 nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
                 if (nq > kWordCap - kWave) {
-                    if (!(diag & 2)) walk_short(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
+                    if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
                     nq = 0;
                 }
             }
         }
     }
-    if (!(diag & 2)) walk_short(wq, nq, lq, nl, mq, nm, prow, plong, crow32, lane);
+    if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
     walk_long(lq, nl, plong, crow32, lane);
-    walk_mid(mq, nm, prow, crow32, lane);
 }
 
 // Phase 3 for one file: lanes = templates (t = lane + 64 j), overlap from the counter row
@@ -441,7 +425,7 @@ __device__ __forceinline__ void prefetch_file(int64_t file, const uint64_t* __re
 
 // Phases 2 + 3, one file per wave (16 waves x 4 files per workgroup). Each wave owns one u32
 // counter row in LDS (zero between files). Narrow words are queued from the file's u64 words
-// >= D and walked (walk_short / walk_mid / walk_long) after the file's dense partials (from
+// >= D and walked (walk_short / walk_long) after the file's dense partials (from
 // dice_post_dense) are added in; scoring reads and re-zeroes the counters and reduces over the
 // wave. The LDS footprint (~74 KiB) and <= 64 VGPRs leave room for two workgroups per CU.
 template <bool kMatrix, int KM>
@@ -459,7 +443,6 @@ __device__ __forceinline__ void post_narrow_body(
     __shared__ uint2 tcs[kPostMaxTpad];                        // packed template constants
     __shared__ uint32_t wq[kPostWaves][kWordCap];              // queued narrow word ids
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
-    __shared__ uint32_t mq[kPostWaves][kMidCap];               // queued mid words
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
@@ -488,7 +471,7 @@ __device__ __forceinline__ void post_narrow_body(
         uint64_t first[kChunks];
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) first[c] = POST_PREFETCH_WORDS ? pre.first[c] : 0;
-        file_postings(row, w64, pb0, first, wq[wave], lq[wave], mq[wave], prow, plong, crow32, lane, diag);
+        file_postings(row, w64, pb0, first, wq[wave], lq[wave], prow, plong, crow32, lane, diag);
         // the wave's next file: its independent loads fly while this one is scored
         if (fi + kPostWaves < kPostFiles && file + kPostWaves < n)
             prefetch_file(file + kPostWaves, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
