@@ -53,7 +53,10 @@ constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
 constexpr int kPostMaxDense = 16;        // dense prefix u64 words (20 / 24 measured slower at T = 600)
 constexpr int kRowW = 16;                // template ids per postings row
-constexpr int kWordCap = 320;            // per-wave queue of narrow word ids
+// per-wave queue of narrow word ids: as long as the narrow kernel's LDS allows two workgroups
+// per CU (counter rows for TPMAX templates beside it)
+template <int TPMAX>
+constexpr int word_cap() { return TPMAX <= 608 ? 416 : 320; }
 constexpr uint16_t kNoTpl = 0xFFFF;      // empty row entry
 constexpr uint16_t kMore = 0xFFFE;       // row entry 15: a long word (entries 0-1 offset, 2 length)
 constexpr int kLongCap = 64;             // per-wave queue of long words (offset, length)
@@ -262,6 +265,7 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 
 // Phase 2 for one file: queue its narrow words (set bits of u64 words >= pb0) and walk their
 // postings into the wave's counter row.
+template <int WCAP>
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
                                               const uint64_t (&first)[kChunks], uint32_t* wq, uint2* lq,
                                               const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -271,7 +275,7 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
 
     // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
     // together. Per chunk a wave prefix sum of the lanes' bit counts gives every lane its
-    // queue slots, and each lane writes its own words (a chunk of more than kWordCap words
+    // queue slots, and each lane writes its own words (a chunk of more than WCAP words
     // -- a file holding most of the vocabulary -- goes round by round instead).
     for (int32_t pb = pb0; pb < w64; pb += kChunks * kWave) {
         uint64_t xs[kChunks];
@@ -288,11 +292,11 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
             const uint32_t incl = wave_incl_scan(cnt);
             const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
             if (total == 0) continue;
-            if (nq + total > kWordCap) {
+            if (nq + total > WCAP) {
                 if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
                 nq = 0;
             }
-            if (total <= kWordCap) {
+            if (total <= WCAP) {
                 uint32_t pos = nq + incl - cnt;
                 while (x) {
                     wq[pos++] = wbase + (uint32_t)__builtin_ctzll(x);
@@ -308,7 +312,7 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
                 const uint64_t bal = __ballot(has);
                 if (has) wq[nq + lane_rank(bal)] = w;
                 nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
-                if (nq > kWordCap - kWave) {
+                if (nq > WCAP - kWave) {
                     if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
                     nq = 0;
                 }
@@ -428,7 +432,7 @@ __device__ __forceinline__ void prefetch_file(int64_t file, const uint64_t* __re
 // >= D and walked (walk_short / walk_long) after the file's dense partials (from
 // dice_post_dense) are added in; scoring reads and re-zeroes the counters and reduces over the
 // wave. The LDS footprint (~74 KiB) and <= 64 VGPRs leave room for two workgroups per CU.
-template <bool kMatrix, int KM>
+template <bool kMatrix, int KM, int TPMAX>
 __device__ __forceinline__ void post_narrow_body(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -438,17 +442,18 @@ __device__ __forceinline__ void post_narrow_body(
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
     // diag (DICE_POST_DIAG, diagnostics only -- results are wrong): 2 skips the postings walk,
     // 4 skips the narrow-word extraction, 8 skips scoring
-    constexpr int kTJ = kPostMaxTpad / kWave;                  // templates per lane
-    __shared__ uint32_t cnt32[kPostWaves * kPostMaxTpad];      // u32 counters, one row per wave
-    __shared__ uint2 tcs[kPostMaxTpad];                        // packed template constants
-    __shared__ uint32_t wq[kPostWaves][kWordCap];              // queued narrow word ids
+    constexpr int kTJ = (TPMAX + kWave - 1) / kWave;           // templates per lane
+    constexpr int kWCap = word_cap<TPMAX>();
+    __shared__ uint32_t cnt32[kPostWaves * TPMAX];             // u32 counters, one row per wave
+    __shared__ uint2 tcs[TPMAX];                               // packed template constants
+    __shared__ uint32_t wq[kPostWaves][kWCap];                 // queued narrow word ids
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
-    uint32_t* crow32 = cnt32 + wave * kPostMaxTpad;
+    uint32_t* crow32 = cnt32 + wave * TPMAX;
     for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
-    for (int i = lane; i < kPostMaxTpad; i += kWave) crow32[i] = 0;
+    for (int i = lane; i < TPMAX; i += kWave) crow32[i] = 0;
     __syncthreads();
 
     const int32_t pb0 = (diag & 4) ? w64 : D;
@@ -471,7 +476,7 @@ __device__ __forceinline__ void post_narrow_body(
         uint64_t first[kChunks];
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) first[c] = POST_PREFETCH_WORDS ? pre.first[c] : 0;
-        file_postings(row, w64, pb0, first, wq[wave], lq[wave], prow, plong, crow32, lane, diag);
+        file_postings<kWCap>(row, w64, pb0, first, wq[wave], lq[wave], prow, plong, crow32, lane, diag);
         // the wave's next file: its independent loads fly while this one is scored
         if (fi + kPostWaves < kPostFiles && file + kPostWaves < n)
             prefetch_file(file + kPostWaves, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
@@ -489,6 +494,7 @@ __device__ __forceinline__ void post_narrow_body(
 
 // Match mode held to 64 VGPRs (8 waves per SIMD: two workgroups per CU); the matrix mode's
 // top-k slots need more registers and run at the occupancy they get.
+template <int TPMAX>
 __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_narrow_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -496,11 +502,11 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
-    post_narrow_body<false, 1>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+    post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, diag, corpus_fast);
 }
 
-template <int KM>
+template <int KM, int TPMAX>
 __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -508,7 +514,7 @@ __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
-    post_narrow_body<true, KM>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+    post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, diag, false);
 }
 
@@ -663,7 +669,8 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
         }
     }
     const int64_t groups = (b->n + kPostFiles - 1) / kPostFiles;
-    auto kern = kMatrix ? dice_post_narrow_matrix<KM> : dice_post_narrow_match;
+    auto kern = c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608> : dice_post_narrow_match<608>)
+                                  : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad> : dice_post_narrow_match<kPostMaxTpad>);
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
