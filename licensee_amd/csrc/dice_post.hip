@@ -26,7 +26,7 @@
 //            4*t into the counter row, 0xFFFF padding) and adds 1 to the first 8 listed
 //            counters (ds_add_u32), words with 9-16 entries their other 8 too; longer ones
 //            wait in a long queue walked by all 64 lanes from the plong array. Scoring
-//            reads (and re-zeroes) the row with lanes = templates (t = lane + 64 j), using the
+//            reads the row with lanes = templates (t = lane + 64 j), using the
 //            packed template constants {len | cc << 31, base | slack << 16}: the same
 //            denominator, IEEE score and strict order (score, then later key) as every other
 //            kernel, 24-bit exact compares inside the fast envelope; match mode reduces over
@@ -324,7 +324,7 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
 }
 
 // Phase 3 for one file: lanes = templates (t = lane + 64 j), overlap from the counter row
-// (re-zeroed for the wave's next file), the shared denominator and order; match
+// (the next file's copy-in overwrites every entry), the shared denominator and order; match
 // mode reduces over the wave, matrix mode writes the row and the top-k.
 template <bool kMatrix, int KM, int TJ>
 __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
@@ -343,7 +343,6 @@ __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, i
         const int32_t t = lane + j * kWave;
         if (t < T) {
             const uint32_t ov = crow32[t];
-            crow32[t] = 0;
             const uint2 pc = tcs[t];   // {len | cc << 31, base | slack << 16}
             const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
                                      (int32_t)(pc.x >> 31));
@@ -430,7 +429,7 @@ __device__ __forceinline__ void prefetch_file(int64_t file, const uint64_t* __re
 // Phases 2 + 3, one file per wave (16 waves x 4 files per workgroup). Each wave owns one u32
 // counter row in LDS (zero between files). Narrow words are queued from the file's u64 words
 // >= D and walked (walk_short / walk_long) after the file's dense partials (from
-// dice_post_dense) are added in; scoring reads and re-zeroes the counters and reduces over the
+// dice_post_dense) are copied in (every entry: no zeroing between files); scoring reads the counters and reduces over the
 // wave. The LDS footprint (~74 KiB) and <= 64 VGPRs leave room for two workgroups per CU.
 template <bool kMatrix, int KM, int TPMAX>
 __device__ __forceinline__ void post_narrow_body(
@@ -481,12 +480,7 @@ __device__ __forceinline__ void post_narrow_body(
         if (fi + kPostWaves < kPostFiles && file + kPostWaves < n)
             prefetch_file(file + kPostWaves, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
 
-        if (diag & 8) {
-#pragma unroll
-            for (int j = 0; j < kTJ; ++j)
-                if (lane + j * kWave < T) crow32[lane + j * kWave] = 0;
-            continue;
-        }
+        if (diag & 8) continue;
         score_file<kMatrix, KM, kTJ>(crow32, tcs, T, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
                                             k, mov, msc, tki, tks, lane);
     }
