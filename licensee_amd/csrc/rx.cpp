@@ -599,6 +599,65 @@ static bool first_list(const NodeP& n, std::vector<char32_t>& out, bool& nullabl
     return out.size() <= kMaxFirst;
 }
 
+// The longest run of consecutive literals on n's mandatory path (a sequence whose items every
+// match consumes in order: literals, groups of them, the first iteration of a repetition with
+// min >= 1); alternations and lookarounds end a run. Every match contains such a run, so a
+// search whose text lacks it from the start position on cannot match.
+struct LitRun {
+    Str s;
+    bool icase = false;
+};
+static void required_runs(const Node* n, LitRun& cur, LitRun& best) {
+    auto flush = [&]() {
+        if (cur.s.size() > best.s.size()) best = cur;
+        cur = LitRun();
+    };
+    switch (n->kind) {
+        case Node::LIT:
+            if (!cur.s.empty() && cur.icase != n->icase) flush();
+            cur.icase = n->icase;
+            cur.s.push_back(n->icase ? fold(n->ch) : n->ch);
+            return;
+        case Node::SEQ:
+            for (auto& k : n->kids) required_runs(k.get(), cur, best);
+            return;
+        case Node::GROUP:
+            required_runs(n->kids[0].get(), cur, best);
+            return;
+        case Node::REPEAT:
+            if (n->min >= 1) {   // the first iteration is mandatory; what follows it is not contiguous
+                flush();
+                required_runs(n->kids[0].get(), cur, best);
+            }
+            flush();
+            return;
+        case Node::BOL: case Node::EOL: case Node::BOS: case Node::EOS: case Node::WORDB:
+            return;   // zero-width: literals on both sides stay adjacent
+        default:      // ANY, CLASS, ALT, LOOK: the run ends here
+            flush();
+            return;
+    }
+}
+
+// first position >= from where req occurs (ASCII case folded when icase), or npos: candidates
+// by a vector scan for the literal's first and last characters (both cases when folded)
+static size_t find_required(const Str& s, size_t from, const Str& req, bool icase) {
+    const size_t m = req.size(), n = s.size();
+    if (m == 0) return from;
+    if (n < m || from > n - m) return Str::npos;
+    auto upper = [&](char32_t c) { return icase && c >= 'a' && c <= 'z' ? c - 32 : c; };
+    const char32_t a = req[0], b = req[m - 1];
+    const char32_t* p = s.data();
+    const size_t last = n - m;
+    for (size_t i = scan::find_pair(p, from, last, m - 1, a, upper(a), b, upper(b)); i <= last;
+         i = scan::find_pair(p, i + 1, last, m - 1, a, upper(a), b, upper(b))) {
+        size_t k = 1;
+        while (k + 1 < m && (icase ? fold(p[i + k]) : p[i + k]) == req[k]) ++k;
+        if (k + 1 >= m) return i;
+    }
+    return Str::npos;
+}
+
 // Zero-width anchor every match of n must begin with: Node::BOS (\A), Node::BOL (^) or -1.
 static int lead_anchor(const Node* n) {
     while (n->kind == Node::GROUP) n = n->kids[0].get();
@@ -629,6 +688,15 @@ Regex::Regex(const std::string& utf8, int flags) {
     if (!ps.eof()) throw std::runtime_error("rx parse: unbalanced )");
     ngroups_ = ps.ngroups;
     index_alternations(root_);
+    {
+        LitRun cur, best;
+        required_runs(root_.get(), cur, best);
+        if (cur.s.size() > best.s.size()) best = cur;
+        if (best.s.size() >= 3) {
+            req_ = best.s;
+            req_icase_ = best.icase;
+        }
+    }
     // Where a match can start: \A-led patterns only at position 0, ^-led patterns only at line
     // starts (every pattern here is re.M). An alternation qualifies when all its branches do.
     const int lead = lead_anchor(root_.get());
@@ -658,6 +726,10 @@ bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
     Matcher mt{s, caps};
     const char32_t* p = s.data();
     const size_t n = s.size();
+    // a match at or after `start` contains req_ at or after `start` (anchored patterns are cheaper
+    // to try at their few start positions)
+    if (!anchored_ && !line_anchored_ && !req_.empty() && find_required(s, start, req_, req_icase_) == Str::npos)
+        return false;
     auto first_ok = [&](char32_t c) { return c < 128 ? first_[c] != 0 : first_nonascii_; };
     for (size_t pos = start; pos <= n; ++pos) {
         if (anchored_ && pos > 0) return false;

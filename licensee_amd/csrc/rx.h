@@ -79,6 +79,8 @@ private:
     bool first_nonascii_ = true;      // ... and whether any non-ASCII one can
     char32_t first_list_[8] = {};     // the exact first-character set when it is this small
     int n_first_list_ = 0;            // (vector scan; 0: use first_)
+    Str req_;                         // a literal every match contains (empty: none found)
+    bool req_icase_ = false;          // ... compared with ASCII case folding
     friend struct Matcher;
 };
 

@@ -61,6 +61,28 @@ inline size_t find_any(const char32_t* p, size_t from, size_t n, const char32_t*
 
 inline size_t find_char(const char32_t* p, size_t from, size_t n, char32_t c) { return find_any(p, from, n, &c, 1); }
 
+// first i in [from, last] with p[i] in {a0, a1} and p[i + d] in {b0, b1}, or last + 1 (the
+// candidate filter of a literal search: its first and last characters, d = length - 1)
+inline size_t find_pair(const char32_t* p, size_t from, size_t last, size_t d, char32_t a0, char32_t a1, char32_t b0,
+                        char32_t b1) {
+    size_t i = from;
+#if defined(__AVX2__)
+    const __m256i va0 = _mm256_set1_epi32((int)a0), va1 = _mm256_set1_epi32((int)a1);
+    const __m256i vb0 = _mm256_set1_epi32((int)b0), vb1 = _mm256_set1_epi32((int)b1);
+    for (; i + 8 <= last + 1; i += 8) {
+        const __m256i x = _mm256_loadu_si256((const __m256i*)(p + i));
+        const __m256i y = _mm256_loadu_si256((const __m256i*)(p + i + d));
+        const __m256i a = _mm256_or_si256(_mm256_cmpeq_epi32(x, va0), _mm256_cmpeq_epi32(x, va1));
+        const __m256i b = _mm256_or_si256(_mm256_cmpeq_epi32(y, vb0), _mm256_cmpeq_epi32(y, vb1));
+        const uint32_t m = lanes(_mm256_and_si256(a, b));
+        if (m) return i + (size_t)__builtin_ctz(m);
+    }
+#endif
+    for (; i <= last; ++i)
+        if ((p[i] == a0 || p[i] == a1) && (p[i + d] == b0 || p[i + d] == b1)) return i;
+    return last + 1;
+}
+
 // index of the second character of the first "  " pair at or after from, or n
 inline size_t find_double_space(const char32_t* p, size_t from, size_t n) {
     size_t i = from;
