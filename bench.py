@@ -292,7 +292,8 @@ def main():
         # into): the H2D runs at the DMA rate instead of through the driver's bounce buffers
         from licensee_amd._native import FileBatch
         pin = lambda a: torch.from_numpy(a).pin_memory().numpy()
-        pfiles = FileBatch(pin(files.bits), pin(files.wordset_size), pin(files.length), pin(files.cc_false_positive))
+        pfw, pln, pcc = pin(files.wordset_size), pin(files.length), pin(files.cc_false_positive)
+        pfiles = FileBatch(pin(files.bits), pfw, pln, pcc)
         torch.cuda.synchronize()
         t_e = time.perf_counter()
         batch.upload(pfiles, sptr)
@@ -300,6 +301,20 @@ def main():
         batch.download_match(sptr)
         extras['e2e_pcie_pinned_files_per_s'] = n_per / (time.perf_counter() - t_e)
         del pfiles
+        # the same files as pinned word-id lists (dice_batch_upload_ids: bitsets built on the
+        # device), fewer bytes over the host link when the vocabulary is large
+        from licensee_amd._native import bits_to_ids
+        offs, ids = bits_to_ids(files.bits, corpus.n_vocab)
+        offs, ids = pin(offs), pin(ids)
+        extras['ids_bytes_per_file'] = round((ids.nbytes + offs.nbytes) / n_per, 1)
+        extras['bitset_bytes_per_file'] = files.bits.shape[1] * 8
+        torch.cuda.synchronize()
+        t_e = time.perf_counter()
+        batch.upload_ids(offs, ids, pfw, pln, pcc, sptr)
+        batch.match(args.threshold, sptr)
+        batch.download_match(sptr)
+        extras['e2e_pcie_ids_pinned_files_per_s'] = n_per / (time.perf_counter() - t_e)
+        del offs, ids
         from licensee_amd.project_files import LicenseFile
         sample = [synth.text(i)[0] for i in range(200)]
         t_h = time.perf_counter()

@@ -20,6 +20,7 @@
  *   dice_*_sharded                  the same two calls with the files sharded over several
  *                                   devices of one node (the dice.rb:34-41 loop is per file)
  *   dice_batch_*                    device-resident batch variants of the two calls above
+ *                                   (inputs as bitsets or as word-id lists)
  *   dice_last_error                 replaces the Ruby exceptions of the path (license.rb:258,
  *                                   content_helper.rb:230,310) with status codes + message
  *
@@ -135,6 +136,16 @@ int dice_batch_create(dice_ctx *ctx, int64_t capacity, dice_batch **out);
 void dice_batch_destroy(dice_batch *batch);
 /* H2D copy + on-device repack of host files into the kernel's tile layout. */
 int dice_batch_upload(dice_batch *batch, const dice_files *files, void *stream);
+/* The same files given as word-id lists instead of bitsets (CSR): file i's ids are
+ * ids[offsets[i] .. offsets[i+1]) as uint16 (id_bytes 2) or uint32 (id_bytes 4) values; the
+ * bitsets are built on the device. Ids >= n_vocab are ignored (words outside the template
+ * vocabulary cannot overlap; they count only in wordset_size), duplicates are harmless.
+ * offsets[0] = 0, non-decreasing (checked). For large vocabularies this moves a fraction of
+ * the bitset bytes over the host link (600 synthetic templates: ~0.6 KB of u16 ids vs 2.9 KB
+ * of bitset per file). Same entry point of the reference as dice_batch_upload. */
+int dice_batch_upload_ids(dice_batch *batch, int64_t n_files, const int64_t *offsets, const void *ids,
+                          int32_t id_bytes, const uint32_t *wordset_size, const int32_t *length,
+                          const uint8_t *cc_false_positive, void *stream);
 /* Kernel-only scoring of the resident batch (asynchronous on `stream`). */
 int dice_batch_match(dice_batch *batch, double threshold, void *stream);
 /* Device-resident matrix results are template-major ([T][n] overlap/score, [k][n] top-k) so

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     'dice_batch_match', 'dice_batch_matrix', 'dice_batch_download_match',
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
     'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
-    'dice_match_sharded', 'dice_similarity_matrix_sharded',
+    'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -69,6 +69,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_create': (ctypes.c_int, [vp, i64, ctypes.POINTER(vp)]),
         'dice_batch_destroy': (None, [vp]),
         'dice_batch_upload': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp]),
+        'dice_batch_upload_ids': (ctypes.c_int, [vp, i64, vp, vp, i32, vp, vp, vp, vp]),
         'dice_batch_match': (ctypes.c_int, [vp, ctypes.c_double, vp]),
         'dice_batch_matrix': (ctypes.c_int, [vp, i32, vp]),
         'dice_batch_download_match': (ctypes.c_int, [vp, vp, vp, vp, vp]),
@@ -129,6 +130,24 @@ class FileBatch:
     def _struct(self) -> _Files:
         return _Files(self.n, _ptr(self.bits), _ptr(self.wordset_size), _ptr(self.length),
                       _ptr(self.cc_false_positive))
+
+
+def bits_to_ids(bits: np.ndarray, n_vocab: int, chunk: int = 16384):
+    """Bitset rows [n, words64(V)] -> the id-list form of ``DeviceBatch.upload_ids``:
+    (offsets [n+1] int64, ids uint16 when V <= 65536 else uint32), ids ascending per file."""
+    bits = np.ascontiguousarray(bits, dtype=np.uint64)
+    n = bits.shape[0]
+    dt = np.uint16 if n_vocab <= 65536 else np.uint32
+    counts = np.zeros(n, np.int64)
+    parts = []
+    for a in range(0, n, chunk):
+        blk = np.unpackbits(bits[a:a + chunk].view(np.uint8), axis=1, bitorder='little')[:, :n_vocab]
+        r, col = np.nonzero(blk)
+        counts[a:a + blk.shape[0]] = np.bincount(r, minlength=blk.shape[0])
+        parts.append(col.astype(dt))
+    offsets = np.zeros(n + 1, np.int64)
+    np.cumsum(counts, out=offsets[1:])
+    return offsets, (np.concatenate(parts) if parts else np.zeros(0, dt))
 
 
 class Scorer:
@@ -220,6 +239,27 @@ class DeviceBatch:
         st = files._struct()
         _check(load_library().dice_batch_upload(self._b, ctypes.byref(st), stream or None))
         self.n = files.n
+
+    def upload_ids(self, offsets: np.ndarray, ids: np.ndarray, wordset_size, length, cc_false_positive,
+                   stream: int = 0):
+        """Upload files as word-id lists (CSR: file i = ids[offsets[i]:offsets[i+1]], uint16 or
+        uint32); the bitsets are built on the device (``dice_batch_upload_ids``)."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        ids = np.ascontiguousarray(ids)
+        if ids.dtype not in (np.uint16, np.uint32):
+            raise ValueError('ids must be uint16 or uint32')
+        wf = np.ascontiguousarray(wordset_size, dtype=np.uint32)
+        ln = np.ascontiguousarray(length, dtype=np.int32)
+        cc = np.ascontiguousarray(cc_false_positive, dtype=np.uint8)
+        n = offsets.shape[0] - 1
+        if n < 0 or not (wf.shape == ln.shape == cc.shape == (n,)):
+            raise ValueError('inconsistent id-list shapes')
+        if n and offsets[-1] > ids.shape[0]:
+            raise ValueError('offsets run past the id list')
+        _check(load_library().dice_batch_upload_ids(self._b, n, _ptr(offsets), _ptr(ids) if ids.size else None,
+                                                    ids.dtype.itemsize, _ptr(wf), _ptr(ln), _ptr(cc),
+                                                    stream or None))
+        self.n = n
 
     def match(self, threshold: float, stream: int = 0):
         _check(load_library().dice_batch_match(self._b, float(threshold), stream or None))

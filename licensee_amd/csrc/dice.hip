@@ -58,6 +58,28 @@ __global__ __launch_bounds__(256) void dice_pack_tiles(const uint64_t* __restric
     tiles[gid] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 
+// Word-id lists -> row-major bitsets: one wave per file builds its row in LDS (ds_or_b64 per
+// id, ids >= V ignored), then writes the whole row (coalesced, every word, zeros included).
+template <class Id>
+__global__ __launch_bounds__(256) void dice_rows_from_ids(const int64_t* __restrict__ offs, const Id* __restrict__ ids,
+                                                          int64_t n, int32_t w64, uint32_t V,
+                                                          uint64_t* __restrict__ rows) {
+    extern __shared__ uint64_t lrow[];   // [4 waves][w64]
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x >> 6;
+    const int64_t file = (int64_t)blockIdx.x * 4 + wave;
+    if (file >= n) return;   // wave-uniform; no block barrier below
+    uint64_t* r = lrow + (size_t)wave * w64;
+    for (int32_t j = lane; j < w64; j += kWave) r[j] = 0;
+    const int64_t a = offs[file], b = offs[file + 1];
+    for (int64_t e = a + lane; e < b; e += kWave) {
+        const uint32_t id = (uint32_t)ids[e];
+        if (id < V) atomicOr(reinterpret_cast<unsigned long long*>(&r[id >> 6]), 1ull << (id & 63));
+    }
+    uint64_t* out = rows + file * w64;
+    for (int32_t j = lane; j < w64; j += kWave) out[j] = r[j];
+}
+
 // [rows][cols] -> [cols][rows] through a padded 64x64 LDS tile (element size 4 or 8 bytes).
 // Used to hand the template-major device matrix back in the ABI's row-major [n][T] layout.
 template <class E>
@@ -384,8 +406,8 @@ int dice_ctx_info(const dice_ctx* ctx, int32_t* T, int32_t* V, int32_t* kind, in
 void dice_batch_destroy(dice_batch* b) {
     if (!b) return;
     DeviceGuard g(b->ctx->device);
-    void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,  b->d_best, b->d_ov,
-                    b->d_score, b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense};
+    void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
+                    b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -418,23 +440,15 @@ int64_t dice_batch_bytes_per_file(const dice_batch* b) {
     return (int64_t)b->ctx->wq * 16;
 }
 
-int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
-    if (!b || !f) return fail(DICE_E_ARG, "NULL batch/files");
+// The per-file scalars and, for the tile-layout kernels, the repack (the rows are in b->d_rows).
+static int upload_tail(dice_batch* b, int64_t n, const uint32_t* wf, const int32_t* len, const uint8_t* cc,
+                       hipStream_t s) {
     dice_ctx* c = b->ctx;
-    if (f->n_files < 0 || f->n_files > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
-    if (f->n_files > 0 && (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive))
-        return fail(DICE_E_ARG, "NULL file arrays");
-    DeviceGuard g(c->device);
-    hipStream_t s = pick_stream(c, stream);
-    const int64_t n = f->n_files;
-    b->n = n;
-    if (n == 0) return DICE_OK;
     const int64_t n_tiles = (n + kWave - 1) / kWave;
     const int64_t npad = n_tiles * kWave;
-    HIP_TRY(hipMemcpyAsync(b->d_rows, f->bits, (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(b->d_wf, f->wordset_size, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(b->d_len, f->length, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(b->d_cc, f->cc_false_positive, (size_t)n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_wf, wf, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_len, len, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_cc, cc, (size_t)n, hipMemcpyHostToDevice, s));
     if (npad > n) {
         HIP_TRY(hipMemsetAsync(b->d_wf + n, 0, (size_t)(npad - n) * 4, s));
         HIP_TRY(hipMemsetAsync(b->d_len + n, 0, (size_t)(npad - n) * 4, s));
@@ -447,6 +461,68 @@ int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
                        c->kind == 1 ? (const int32_t*)c->d_qperm : nullptr, b->d_tiles, n_tiles);
     HIP_TRY(hipGetLastError());
     return DICE_OK;
+}
+
+int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
+    if (!b || !f) return fail(DICE_E_ARG, "NULL batch/files");
+    dice_ctx* c = b->ctx;
+    if (f->n_files < 0 || f->n_files > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
+    if (f->n_files > 0 && (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive))
+        return fail(DICE_E_ARG, "NULL file arrays");
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    const int64_t n = f->n_files;
+    b->n = n;
+    if (n == 0) return DICE_OK;
+    HIP_TRY(hipMemcpyAsync(b->d_rows, f->bits, (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, s));
+    return upload_tail(b, n, f->wordset_size, f->length, f->cc_false_positive, s);
+}
+
+int dice_batch_upload_ids(dice_batch* b, int64_t n, const int64_t* offsets, const void* ids, int32_t id_bytes,
+                          const uint32_t* wordset_size, const int32_t* length, const uint8_t* cc, void* stream) {
+    if (!b) return fail(DICE_E_ARG, "NULL batch");
+    dice_ctx* c = b->ctx;
+    if (n < 0 || n > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
+    if (id_bytes != 2 && id_bytes != 4) return fail(DICE_E_ARG, "id_bytes must be 2 or 4");
+    if (n > 0 && (!offsets || !wordset_size || !length || !cc)) return fail(DICE_E_ARG, "NULL file arrays");
+    if (n > 0) {
+        if (offsets[0] != 0) return fail(DICE_E_ARG, "offsets[0] must be 0");
+        for (int64_t i = 0; i < n; ++i)
+            if (offsets[i + 1] < offsets[i]) return fail(DICE_E_ARG, "offsets must be non-decreasing");
+        if (offsets[n] > 0 && !ids) return fail(DICE_E_ARG, "NULL ids");
+    }
+    if ((int64_t)c->w64 * 8 * 4 > 64 * 1024) return fail(DICE_E_ARG, "vocabulary too large for id upload");
+    DeviceGuard g(c->device);
+    hipStream_t s = pick_stream(c, stream);
+    b->n = n;
+    if (n == 0) return DICE_OK;
+    const size_t need = (size_t)std::max<int64_t>(offsets[n], 1) * (size_t)id_bytes;
+    if (need > b->ids_bytes) {
+        HIP_TRY(hipStreamSynchronize(s));   // the staging may still feed an earlier upload
+        if (b->d_ids) (void)hipFree(b->d_ids);
+        b->d_ids = nullptr;
+        b->ids_bytes = 0;
+        int rc = dalloc_bytes(&b->d_ids, need);
+        if (rc) return rc;
+        b->ids_bytes = need;
+    }
+    if (!b->d_offs) {
+        int rc = dalloc_bytes(reinterpret_cast<void**>(&b->d_offs), (size_t)(b->capacity + 1) * 8);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(b->d_offs, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (offsets[n] > 0)
+        HIP_TRY(hipMemcpyAsync(b->d_ids, ids, (size_t)offsets[n] * (size_t)id_bytes, hipMemcpyHostToDevice, s));
+    const unsigned grid = (unsigned)((n + 3) / 4);
+    const size_t lds = (size_t)4 * c->w64 * 8;
+    if (id_bytes == 2)
+        hipLaunchKernelGGL(dice_rows_from_ids<uint16_t>, dim3(grid), dim3(256), lds, s, b->d_offs,
+                           (const uint16_t*)b->d_ids, n, c->w64, (uint32_t)c->V, b->d_rows);
+    else
+        hipLaunchKernelGGL(dice_rows_from_ids<uint32_t>, dim3(grid), dim3(256), lds, s, b->d_offs,
+                           (const uint32_t*)b->d_ids, n, c->w64, (uint32_t)c->V, b->d_rows);
+    HIP_TRY(hipGetLastError());
+    return upload_tail(b, n, wordset_size, length, cc, s);
 }
 
 int dice_batch_match(dice_batch* b, double thr, void* stream) {

@@ -102,6 +102,9 @@ struct dice_batch {
     double* d_tks = nullptr;
     void* d_stage = nullptr;        // row-major staging for downloads
     void* d_pdense = nullptr;       // kind 3: dense-prefix partial overlaps [capacity][tp] u16
+    void* d_ids = nullptr;          // dice_batch_upload_ids staging: the id list ...
+    size_t ids_bytes = 0;
+    int64_t* d_offs = nullptr;      // ... and its [capacity + 1] offsets
     size_t pdense_bytes = 0;
     size_t stage_bytes = 0;
 };

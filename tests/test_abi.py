@@ -62,6 +62,8 @@ def test_sharded_calls_reject_bad_arguments():
     assert b'NULL ctx' in lib.dice_last_error()
     assert lib.dice_similarity_matrix_sharded(ctxs, 1, ctypes.byref(f), 7, None, None, 0, None, None) == -1
     assert b'gather_mode' in lib.dice_last_error()
+    assert lib.dice_batch_upload_ids(None, 0, None, None, 2, None, None, None, None) == -1
+    assert b'NULL batch' in lib.dice_last_error()
 
 
 def test_no_cpu_fallback_without_gpu():
@@ -133,3 +135,19 @@ def test_vocab_pack_is_a_permutation_and_never_worse():
         bad = init.copy()
         bad[0] = bad[1]
         assert fn(sig.ctypes.data, V, W, T, bad.ctypes.data, bin_bits, 10, 7, out.ctypes.data) == -1
+
+
+def test_bits_to_ids_round_trip():
+    """_native.bits_to_ids (the id-list form of dice_batch_upload_ids) lists each row's set bits
+    in ascending order, uint16 up to 65,536 words, across chunk boundaries and empty rows."""
+    rng = np.random.default_rng(3)
+    for V, n, chunk in ((1000, 300, 70), (70000, 40, 16)):
+        dense = rng.random((n, V)) < 0.01
+        dense[5] = False
+        pad = np.pad(dense, ((0, 0), (0, (-V) % 64)))
+        bits = np.packbits(pad, axis=1, bitorder='little').view(np.uint64)
+        offs, ids = _native.bits_to_ids(bits, V, chunk=chunk)
+        assert ids.dtype == (np.uint16 if V <= 65536 else np.uint32)
+        assert offs[0] == 0 and offs[-1] == ids.size
+        for r in range(n):
+            assert np.array_equal(ids[offs[r]:offs[r + 1]], np.flatnonzero(dense[r]))
