@@ -85,13 +85,19 @@ typedef struct dice_files {
 int32_t dice_words64(int32_t n_vocab);
 
 /* Upload a template corpus to `device` (HIP ordinal). Selects the kernel for the corpus
- * (template-specialized sparse program for T <= 64, dense tiled otherwise). */
+ * (template-specialized sparse program for T <= 64; postings kernels, LDS record kernel or
+ * dense tiles above). */
 int dice_create(const dice_templates *templates, int32_t device, dice_ctx **out);
 void dice_destroy(dice_ctx *ctx);
 
-/* Introspection: T, V, kernel kind (0 = dense, 1 = sparse program), program entries. */
+/* Introspection: T, V, kernel kind (0 = dense, 1 = sparse program, 2 = LDS records,
+ * 3 = postings), program entries. */
 int dice_ctx_info(const dice_ctx *ctx, int32_t *n_templates, int32_t *n_vocab,
                   int32_t *kernel_kind, int32_t *program_entries);
+/* Introspection: the kernel dice_match / dice_batch_match run -- the kernel kind above, or
+ * 4 = bound-pruned match (kind 3 corpora; DICE_POST_PRUNE=0 keeps the postings kernels) --
+ * or -1 for a NULL ctx. Results are identical whichever runs. */
+int32_t dice_ctx_match_kernel(const dice_ctx *ctx);
 
 /* Dice#match / #confidence for every file, synchronous, host buffers.
  *   best[i]    index of the matched template, or -1 (Dice#match nil) when the top

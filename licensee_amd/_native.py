@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = (
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
     'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
     'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids',
+    'dice_ctx_match_kernel',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -64,6 +65,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_create': (ctypes.c_int, [ctypes.POINTER(_Templates), i32, ctypes.POINTER(vp)]),
         'dice_destroy': (None, [vp]),
         'dice_ctx_info': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        'dice_ctx_match_kernel': (ctypes.c_int32, [vp]),
         'dice_match': (ctypes.c_int, [vp, ctypes.POINTER(_Files), ctypes.c_double, vp, vp, vp]),
         'dice_similarity_matrix': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp, vp, i32, vp, vp]),
         'dice_batch_create': (ctypes.c_int, [vp, i64, ctypes.POINTER(vp)]),
@@ -186,6 +188,11 @@ class Scorer:
         vals = [ctypes.c_int32() for _ in range(4)]
         _check(load_library().dice_ctx_info(self._ctx, *[ctypes.byref(v) for v in vals]))
         return tuple(v.value for v in vals)
+
+    def match_kernel(self) -> int:
+        """Kernel Dice#match runs on: 0 dense, 1 sparse program, 2 LDS records, 3 postings,
+        4 bound-pruned (dice_prune.hip)."""
+        return int(load_library().dice_ctx_match_kernel(self._ctx))
 
     def match(self, files: FileBatch, threshold: float):
         n = files.n

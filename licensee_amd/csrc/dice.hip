@@ -306,7 +306,8 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
-    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc};
+    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc,
+                    c->d_qa, c->d_qoff, c->d_qrec};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -374,7 +375,10 @@ int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
         const char* pick = getenv("DICE_LARGE_KERNEL");
         const std::string want = pick && *pick ? pick : "post";
         if (!(force && *force == '1') && want != "dense") {
-            if (want == "post" && dice::post_feasible(t)) rc = dice::post_setup(c, t);
+            if (want == "post" && dice::post_feasible(t)) {
+                rc = dice::post_setup(c, t);
+                if (rc == DICE_OK) rc = dice::prune_setup(c, t);   // match mode (DICE_POST_PRUNE=0: off)
+            }
             else rc = dice::lds_setup(c, t);
         }
     }
@@ -401,6 +405,11 @@ int dice_ctx_info(const dice_ctx* ctx, int32_t* T, int32_t* V, int32_t* kind, in
         *entries = ctx->kind == 2 ? (int32_t)ctx->lds_entries
                  : ctx->kind == 3 ? (int32_t)ctx->post_rows : (int32_t)ctx->prog.entries();
     return DICE_OK;
+}
+
+int32_t dice_ctx_match_kernel(const dice_ctx* ctx) {
+    if (!ctx) return -1;
+    return ctx->kind == 3 && ctx->prune ? 4 : ctx->kind;
 }
 
 void dice_batch_destroy(dice_batch* b) {
@@ -540,7 +549,7 @@ int dice_batch_match(dice_batch* b, double thr, void* stream) {
         int rc = dice::lds_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else if (c->kind == 3) {
-        int rc = dice::post_launch_match(c, b, thr, s);
+        int rc = c->prune ? dice::prune_launch_match(c, b, thr, s) : dice::post_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,

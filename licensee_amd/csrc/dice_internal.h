@@ -61,6 +61,13 @@ struct dice_ctx {
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0;
     bool post_fast = false;
     int64_t post_rows = 0;
+    // kind 3 match mode, bound-pruned (dice_prune.hip): per-template group counts, records
+    void* d_qa = nullptr;      // [T][kPruneGroups / 2] u32: |Lf ∩ group g| as u16 pairs
+    void* d_qoff = nullptr;    // [T + 1] u32 record offsets
+    void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
+    bool prune = false;
+    int32_t prune_sched = 0;
+    int64_t prune_records = 0;
 };
 
 namespace dice {
@@ -70,6 +77,8 @@ bool post_feasible(const dice_templates* t);
 int post_setup(dice_ctx* c, const dice_templates* t);
 int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s);
+int prune_setup(dice_ctx* c, const dice_templates* t);
+int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
 // the ctx's reusable batch for the host-buffer calls (grown on demand)
 int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out);
 // result downloads to host memory or (kind hipMemcpyDefault) another device's memory;

@@ -39,6 +39,7 @@
 
 #include "dice_common.h"
 #include "dice_internal.h"
+#include "dice_wave.h"
 
 namespace dice {
 
@@ -61,53 +62,6 @@ constexpr uint16_t kNoTpl = 0xFFFF;      // empty row entry
 constexpr uint16_t kMore = 0xFFFE;       // row entry 15: a long word (entries 0-1 offset, 2 length)
 constexpr int kLongCap = 64;             // per-wave queue of long words (offset, length)
 constexpr int kChunks = 3;               // 64-word chunks of a file loaded together
-
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// "a ranks at or above b" in score order. FAST: both overlaps < 2^11 and both denominators in
-// [1, 2^21) with scores < 1024 (the file and corpus envelope checked by the caller), where
-// the rational compare is exact in 24-bit multiplies and equals the double order (dice_common.h).
-template <bool FAST>
-__device__ __forceinline__ bool ge(uint32_t oa, int32_t da, uint32_t ob, int32_t db) {
-    if (FAST) return __umul24(oa, (uint32_t)db) >= __umul24(ob, (uint32_t)da);
-    return dice_ge(oa, da, ob, db);
-}
-
-template <bool FAST>
-__device__ __forceinline__ bool outranks_t(int32_t ai, uint32_t ao, int32_t ad, int32_t bi, uint32_t bo, int32_t bd) {
-    if (ai < 0) return false;
-    if (bi < 0) return true;
-    const bool g = ge<FAST>(ao, ad, bo, bd), l = ge<FAST>(bo, bd, ao, ad);
-    return g && (!l || ai > bi);
-}
-
-// Wave-wide argmax of (idx, ov, den) under `outranks` (butterfly over all 64 lanes).
-template <bool FAST = false>
-__device__ __forceinline__ void wave_best(int32_t& bi, uint32_t& bo, int32_t& bd) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const int32_t oi = __shfl_xor(bi, m);
-        const uint32_t oo = (uint32_t)__shfl_xor((int)bo, m);
-        const int32_t od = __shfl_xor(bd, m);
-        if (outranks_t<FAST>(oi, oo, od, bi, bo, bd)) { bi = oi; bo = oo; bd = od; }
-    }
-}
-
-// Inclusive prefix sum over the 64 lanes (DPP: row shifts within each 16-lane row, then the
-// row-15 / row-31 broadcasts); every lane must be active.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);   // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-
-__device__ __forceinline__ uint32_t lane_rank(uint64_t bal) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-}
 
 // Postings entries are byte offsets (4 * template) into the wave's u32 counter row.
 __device__ __forceinline__ void count(uint32_t* crow32, uint32_t off) {

@@ -1,0 +1,306 @@
+// Bound-pruned Dice#match for large template sets (kind 3, T > 64; BASELINE config 3).
+//
+// Same contract as every match kernel (dice.rb:8-14,34-48 over content_helper.rb:128-133,
+// 337-347): per file the top template among the unmasked ones in the strict (score, later key)
+// order, its overlap and f64 score, and the index when score >= threshold. Only the top
+// template's score leaves the kernel, so a template whose score provably cannot reach the top
+// need not be scored exactly (the MaxScore idea of inverted-index retrieval):
+//
+//   ov_t = |Lf_t ∩ W_F| <= m_t = sum over word groups g of min(|Lf_t ∩ g|, |W_F ∩ g|)
+//
+// with 16 groups of vocabulary u64 words (word p is in group (p mod 64) / 4, so a lane's words
+// all fall in one group and the file's group counts are a 4-lane sum). The score is monotone
+// in the overlap (den > 0), so bound_t = (m_t * 200.0) / den_t >= score_t in IEEE doubles.
+// Per file (one wave): all T bounds (lanes = templates, packed u16 min/add over the groups),
+// then repeatedly score exactly the template of largest bound -- its records {u64 word, mask}
+// against the file's row in LDS, one lane per record -- and drop every template whose bound is
+// below the best score so far, until none is left. A dropped template scores strictly below
+// the winner, and every template tying or beating it has bound >= its score, so it is scored:
+// the winner, overlap and score are those of the full scan. Ordering uses f32 bounds rounded
+// UP (keys); only the drop test matters for correctness and it compares an upper bound of the
+// bound against a lower bound of the best score. Templates with den <= 0 are never dropped.
+//
+// On the config-3 workload a file scores 1.4 templates exactly on average (p99 13, of 600):
+// the per-file cost is the bound pass, not the overlap. Files that resemble no template (low
+// best score, loose bounds) score more templates, at worst all of them -- the same records
+// walk as the LDS kernel (dice_lds.hip); the results never change. Matrix/top-k mode keeps the
+// postings kernels (dice_post.hip): it needs every score.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "dice_common.h"
+#include "dice_internal.h"
+#include "dice_wave.h"
+
+namespace dice {
+
+constexpr int kPruneWaves = 16;          // waves per workgroup
+constexpr int kPruneFPW = 4;             // files per wave
+constexpr int kPruneGroups = 16;         // word groups of the bound (u16 pairs: 8 dwords per template)
+constexpr int kPruneMaxJ = 8;            // u64 words per lane: w64 <= 512 (V <= 32768)
+constexpr int kPruneMaxT = 704;          // = kPostMaxTpad (the key's low 10 bits hold the template)
+constexpr uint32_t kKeyLow = 1023u;
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_min_add(uint32_t acc, uint32_t a, uint32_t f) {
+    const u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, f));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, acc) + m);
+}
+
+// The next file's independent loads, in flight while the wave works on the current file.
+template <int J>
+struct PruneNext {
+    uint64_t w[J];
+    uint32_t wf, cc;
+    int32_t lf;
+};
+
+template <int J>
+__device__ __forceinline__ void prune_load(PruneNext<J>& nx, const uint64_t* __restrict__ rows, int64_t file,
+                                           int32_t w64, const uint32_t* __restrict__ wfp,
+                                           const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp,
+                                           int lane) {
+    const uint64_t* row = rows + file * w64;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int32_t p = lane + j * kWave;
+        nx.w[j] = p < w64 ? __builtin_nontemporal_load(row + p) : 0;
+    }
+    nx.wf = wfp[file];
+    nx.lf = lenp[file];
+    nx.cc = ccp[file];
+}
+
+// f32 upper bound of (m * 200.0) / den rounded up to the key grid (low 10 bits = template).
+// The relative error of the f32 evaluation (conversions, v_rcp_f32, two products) is < 2^-20;
+// the 1 + 2^-16 factor covers it, and the key rounding only raises the value further.
+__device__ __forceinline__ uint32_t bound_key(uint32_t m, int32_t den, int32_t t) {
+    if (den <= 0) return 0x7F800000u | (uint32_t)t;   // +inf: never dropped
+    const float fb = (float)m * 200.0f * __builtin_amdgcn_rcpf((float)den) * 1.0000153f;
+    const uint32_t kb = max((__float_as_uint(fb) + kKeyLow) & ~kKeyLow, kKeyLow + 1);
+    return kb | (uint32_t)t;
+}
+
+template <int J, int TJ, int NW, bool PF, int OCC>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void dice_prune_match(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint32_t* __restrict__ qa,
+    const uint2* __restrict__ tc, const uint32_t* __restrict__ qoff, const uint4* __restrict__ qrec,
+    const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
+    int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast) {
+    // LDS: [waves][w64] file rows | [T][8] group counts | [T] packed constants | [T + 1] record offsets
+    extern __shared__ uint64_t lds[];
+    uint32_t* sqa = reinterpret_cast<uint32_t*>(lds + (size_t)NW * w64);
+    uint2* stc = reinterpret_cast<uint2*>(sqa + (size_t)T * (kPruneGroups / 2));
+    uint32_t* soff = reinterpret_cast<uint32_t*>(stc + T);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    uint64_t* myrow = lds + (size_t)wave * w64;
+    for (int i = threadIdx.x; i < T * (kPruneGroups / 2); i += NW * kWave) sqa[i] = qa[i];
+    for (int i = threadIdx.x; i < T; i += NW * kWave) stc[i] = tc[i];
+    for (int i = threadIdx.x; i <= T; i += NW * kWave) soff[i] = qoff[i];
+
+    const int64_t f0 = (int64_t)blockIdx.x * (NW * kPruneFPW) + wave;
+    PruneNext<J> nx;
+    if (PF && f0 < n) prune_load<J>(nx, rows, f0, w64, wfp, lenp, ccp, lane);
+    __syncthreads();
+
+    for (int i = 0; i < kPruneFPW; ++i) {
+        const int64_t file = f0 + (int64_t)i * NW;
+        if (file >= n) break;   // wave-uniform
+        if (!PF) prune_load<J>(nx, rows, file, w64, wfp, lenp, ccp, lane);
+        // the file's row into the wave's LDS row; per-lane bit counts
+        uint32_t pc = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int32_t p = lane + j * kWave;
+            if (p < w64) myrow[p] = nx.w[j];
+            pc += (uint32_t)__builtin_popcountll(nx.w[j]);
+        }
+        const uint32_t wf = nx.wf;
+        const int32_t lf = nx.lf;
+        const bool ccf = nx.cc != 0;
+        if (PF && i + 1 < kPruneFPW && file + NW < n)
+            prune_load<J>(nx, rows, file + NW, w64, wfp, lenp, ccp, lane);
+        // group g = lane / 4: 4-lane sums (DPP quad_perm), packed two groups per dword
+        pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+        pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+        uint32_t fg[kPruneGroups / 2];
+#pragma unroll
+        for (int k = 0; k < kPruneGroups / 2; ++k)
+            fg[k] = rfl(__builtin_amdgcn_readlane(pc, 8 * k) | (__builtin_amdgcn_readlane(pc, 8 * k + 4) << 16));
+
+        // bounds of every unmasked template (lanes = templates t = lane + 64 j)
+        uint32_t key[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const int32_t t = lane + j * kWave;
+            key[j] = 0;
+            if (t < T) {
+                const uint2 c = stc[t];   // {len | cc << 31, base | slack << 16}
+                if (!((c.x >> 31) && ccf)) {
+                    const uint4 a0 = *reinterpret_cast<const uint4*>(sqa + (size_t)t * 8);
+                    const uint4 a1 = *reinterpret_cast<const uint4*>(sqa + (size_t)t * 8 + 4);
+                    uint32_t acc = 0;
+                    acc = pk_min_add(acc, a0.x, fg[0]);
+                    acc = pk_min_add(acc, a0.y, fg[1]);
+                    acc = pk_min_add(acc, a0.z, fg[2]);
+                    acc = pk_min_add(acc, a0.w, fg[3]);
+                    acc = pk_min_add(acc, a1.x, fg[4]);
+                    acc = pk_min_add(acc, a1.y, fg[5]);
+                    acc = pk_min_add(acc, a1.z, fg[6]);
+                    acc = pk_min_add(acc, a1.w, fg[7]);
+                    const uint32_t m = (acc & 0xFFFFu) + (acc >> 16);
+                    const int32_t den = dice_den(make_int4((int32_t)(c.y & 0xFFFFu), (int32_t)c.y >> 16,
+                                                           (int32_t)(c.x & 0x7FFFFFFFu), 0), wf, lf);
+                    key[j] = bound_key(m, den, t);
+                }
+            }
+        }
+        // the file's row is read by other lanes below: LDS ops of a wave run in order
+        __builtin_amdgcn_wave_barrier();
+
+        const bool fast = corpus_fast && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
+        int32_t bi = -1, bd = 1;
+        uint32_t bo = 0;
+        float llo = -1.0f;   // lower bound of the best score (f32); bounds below it are dropped
+        for (;;) {
+            uint32_t km = 0;
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                if (__uint_as_float(key[j] & ~kKeyLow) < llo) key[j] = 0;
+                km = max(km, key[j]);
+            }
+            const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
+            if (K == 0) break;   // every template scored or dropped
+            const int32_t ts = (int32_t)(K & kKeyLow);
+            if (lane == (ts & (kWave - 1))) {
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+                    if (j == (ts >> 6)) key[j] = 0;
+            }
+            // exact overlap: one lane per record of template ts, two records per lane in flight
+            const uint32_t r0 = rfl(soff[ts]), r1 = rfl(soff[ts + 1]);
+            uint32_t acc = 0;
+            for (uint32_t r = r0 + lane; r < r1; r += 2 * kWave) {
+                const uint4 a = qrec[r];
+                const uint4 b = r + kWave < r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+                const uint64_t fa = myrow[a.x], fb = myrow[b.x];
+                acc += (uint32_t)__builtin_popcount((uint32_t)fa & a.y) + (uint32_t)__builtin_popcount((uint32_t)(fa >> 32) & a.z);
+                acc += (uint32_t)__builtin_popcount((uint32_t)fb & b.y) + (uint32_t)__builtin_popcount((uint32_t)(fb >> 32) & b.z);
+            }
+            const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
+            const uint2 c = stc[ts];
+            const int32_t den = dice_den(make_int4((int32_t)(c.y & 0xFFFFu), (int32_t)c.y >> 16,
+                                                   (int32_t)(c.x & 0x7FFFFFFFu), 0), wf, lf);
+            const bool better = fast ? outranks_t<true>(ts, ov, den, bi, bo, bd) : outranks_t<false>(ts, ov, den, bi, bo, bd);
+            if (better) {
+                bi = ts;
+                bo = ov;
+                bd = den;
+                const double s = dice_score(bo, bd);
+                // f32 lower bound of s: (1 - 2^-16) s rounds to nearest below s; no dropping
+                // against a non-positive or NaN best
+                llo = s > 0.0 ? (float)(s * (1.0 - 1.0 / 65536.0)) : -1.0f;
+            }
+        }
+        if (lane == 0) {
+            const double s = bi >= 0 ? dice_score(bo, bd) : 0.0;
+            best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
+            ov_out[file] = bo;
+            score_out[file] = s;
+        }
+    }
+}
+
+// ---- host side ---------------------------------------------------------------------------
+
+static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
+    return (size_t)nw * w64 * 8 + (size_t)T * (kPruneGroups / 2) * 4 + (size_t)T * 8 + ((size_t)T + 1) * 4;
+}
+
+int prune_setup(dice_ctx* c, const dice_templates* t) {
+    const char* e = getenv("DICE_POST_PRUNE");
+    if (e && *e == '0') return DICE_OK;
+    const int32_t T = c->T, w64 = c->w64;
+    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024) return DICE_OK;
+    // group counts |Lf_t ∩ g| (< 2^16: post_feasible bounds |Lf|), records of nonzero u64 words
+    std::vector<uint32_t> qa((size_t)T * (kPruneGroups / 2), 0);
+    std::vector<uint32_t> qoff((size_t)T + 1, 0);
+    std::vector<uint4> qrec;
+    for (int32_t i = 0; i < T; ++i) {
+        const uint64_t* r = t->lf_bits + (size_t)i * w64;
+        uint32_t g16[kPruneGroups] = {0};
+        for (int32_t p = 0; p < w64; ++p) {
+            if (!r[p]) continue;
+            g16[(p % kWave) / 4] += (uint32_t)__builtin_popcountll(r[p]);
+            qrec.push_back(make_uint4((uint32_t)p, (uint32_t)r[p], (uint32_t)(r[p] >> 32), 0));
+        }
+        for (int k = 0; k < kPruneGroups / 2; ++k) qa[(size_t)i * 8 + k] = g16[2 * k] | (g16[2 * k + 1] << 16);
+        qoff[(size_t)i + 1] = (uint32_t)qrec.size();
+    }
+    if (qrec.empty()) qrec.push_back(make_uint4(0, 0, 0, 0));
+    int rc;
+    if ((rc = dalloc_bytes(&c->d_qa, qa.size() * 4)) || (rc = dalloc_bytes(&c->d_qoff, qoff.size() * 4)) ||
+        (rc = dalloc_bytes(&c->d_qrec, qrec.size() * sizeof(uint4))))
+        return rc;
+    if (hipMemcpy(c->d_qa, qa.data(), qa.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_qoff, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_qrec, qrec.data(), qrec.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(DICE_E_DEVICE, "pruned-match plan upload failed");
+    c->prune_records = (int64_t)qoff[(size_t)T];
+    const char* sc = getenv("DICE_PRUNE_SCHED");
+    c->prune_sched = sc && *sc ? atoi(sc) : 0;
+    c->prune = true;
+    return DICE_OK;
+}
+
+template <int J, int TJ, int NW, bool PF, int OCC>
+static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
+    auto kern = dice_prune_match<J, TJ, NW, PF, OCC>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
+    const int64_t groups = (b->n + NW * kPruneFPW - 1) / (NW * kPruneFPW);
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows,
+                       b->n, c->w64, c->T, (const uint32_t*)c->d_qa, (const uint2*)c->d_ptc,
+                       (const uint32_t*)c->d_qoff, (const uint4*)c->d_qrec, b->d_wf, b->d_len, b->d_cc, thr,
+                       b->d_best, b->d_ov, b->d_score, c->post_fast);
+    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
+}
+
+// Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, row loads at the file;
+// 1 = 8-wave workgroups, the next file's row prefetched in VGPRs (6 waves/SIMD);
+// 2 = 8-wave workgroups, row loads at the file (8 waves/SIMD).
+template <int J, int TJ>
+static int launch_prune_s(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    switch (c->prune_sched) {
+        case 1: return launch_prune<J, TJ, 8, true, 6>(c, b, thr, s);
+        case 2: return launch_prune<J, TJ, 8, false, 8>(c, b, thr, s);
+        default: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
+    }
+}
+
+template <int J>
+static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    return c->T <= 640 ? launch_prune_s<J, 10>(c, b, thr, s)
+                       : launch_prune_s<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
+}
+
+int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    if (b->n == 0) return DICE_OK;
+    switch ((c->w64 + kWave - 1) / kWave) {
+        case 1: return launch_prune_j<1>(c, b, thr, s);
+        case 2: return launch_prune_j<2>(c, b, thr, s);
+        case 3:
+        case 4: return launch_prune_j<4>(c, b, thr, s);
+        case 5:
+        case 6: return launch_prune_j<6>(c, b, thr, s);
+        default: return launch_prune_j<8>(c, b, thr, s);
+    }
+}
+
+}  // namespace dice

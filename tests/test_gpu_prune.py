@@ -1,0 +1,177 @@
+"""GPU parity of the bound-pruned match kernel (licensee_amd/csrc/dice_prune.hip).
+
+For large corpora (T > 64) Dice#match (dice.rb:8-14,34-48) runs a kernel that scores exactly
+only the templates whose overlap bound can still reach the best score. Its outputs -- best
+index, overlap and score -- must equal the full scan's. Checked bit-exact against the C oracle's
+hash mode (the Set#& restatement of content_helper.rb:128-133) and against the postings kernel
+(DICE_POST_PRUNE=0), on:
+
+  * the config-3 corpus (600 synthetic templates, V = 23,494) and its synthetic files;
+  * files that resemble no template (random bitsets: loose bounds, many exact scores), empty
+    files, CC-flagged files, files outside the fast envelope (|W_F| >= 2^20, len_F >= 2^21);
+  * exact ties: duplicated templates, where the later key must win (dice.rb:39);
+  * a tiny vocabulary (one u64 word per lane) and T = 700 (11 templates per lane);
+  * every schedule variant (DICE_PRUNE_SCHED) and ragged batch sizes.
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import ArrayCorpus, widen_lanes
+
+pytestmark = pytest.mark.gpu
+
+
+def _scorer(c):
+    from licensee_amd._native import Scorer
+    return Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab, device=0)
+
+
+def _oracle(c):
+    from oracle.native import OracleScorer
+    return OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
+
+
+def _match_all(c, fb, thresholds, monkeypatch, sched=None):
+    """Match results of the pruned kernel and of the postings kernel, per threshold."""
+    out = {}
+    for prune in ('1', '0'):
+        monkeypatch.setenv('DICE_POST_PRUNE', prune)
+        if sched is not None:
+            monkeypatch.setenv('DICE_PRUNE_SCHED', str(sched))
+        sc = _scorer(c)
+        try:
+            assert sc.info()[2] == 3
+            assert sc.match_kernel() == (4 if prune == '1' else 3)
+            out[prune] = {thr: sc.match(fb, thr) for thr in thresholds}
+        finally:
+            sc.close()
+    monkeypatch.delenv('DICE_POST_PRUNE', raising=False)
+    monkeypatch.delenv('DICE_PRUNE_SCHED', raising=False)
+    return out['1'], out['0']
+
+
+def _assert_same(got, exp, where):
+    best, ov, score = got
+    eb, eo, es = exp
+    assert np.array_equal(ov, eo), (where, np.nonzero(ov != eo)[0][:10])
+    assert np.array_equal(score, es), (where, np.nonzero(score != es)[0][:10])
+    assert np.array_equal(best, eb), (where, np.nonzero(best != eb)[0][:10])
+
+
+def _check(c, fb, monkeypatch, thresholds=(98.0, 0.0, 100.5), sched=None):
+    pruned, full = _match_all(c, fb, thresholds, monkeypatch, sched)
+    orc = _oracle(c)
+    for thr in thresholds:
+        exp = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, thr, nthreads=16, mode=0)
+        _assert_same(pruned[thr], exp, ('pruned vs oracle', thr))
+        _assert_same(full[thr], exp, ('postings vs oracle', thr))
+    return pruned
+
+
+@pytest.fixture(scope='module')
+def config3():
+    import bench
+    from licensee_amd.synth import SyntheticCorpus
+    c = bench.build_workload(3)
+    fb = SyntheticCorpus(c).generate(0, 30000, seed=20250202, nthreads=16)
+    return c, fb
+
+
+def test_config3_files(config3, monkeypatch):
+    c, fb = config3
+    res = _check(c, fb, monkeypatch)
+    best, ov, score = res[98.0]
+    assert 0.3 < np.mean(best >= 0) < 0.9   # the workload matches some files, not all
+
+
+@pytest.mark.parametrize('sched', [0, 1, 2])
+@pytest.mark.parametrize('n', [1, 63, 64, 65, 129, 1000])
+def test_schedules_and_ragged_batches(config3, sched, n, monkeypatch):
+    from licensee_amd._native import FileBatch
+    c, fb = config3
+    lo = 517
+    part = FileBatch(fb.bits[lo:lo + n], fb.wordset_size[lo:lo + n], fb.length[lo:lo + n],
+                     fb.cc_false_positive[lo:lo + n])
+    _check(c, part, monkeypatch, thresholds=(98.0, 0.0), sched=sched)
+
+
+def _random_files(c, n, seed, density):
+    """Files that resemble no template: random vocabulary bits at a given density, |W_F| the
+    in-vocabulary count plus random out-of-vocabulary words, random lengths, 30% CC-flagged,
+    every 17th file empty."""
+    from licensee_amd._native import FileBatch
+    rng = np.random.default_rng(seed)
+    V = c.n_vocab
+    w64 = (V + 63) // 64
+    bits = np.zeros((n, w64), np.uint64)
+    dens = rng.uniform(0, density, n)
+    for i in range(n):
+        ids = np.nonzero(rng.random(V) < dens[i])[0]
+        np.bitwise_or.at(bits[i], ids // 64, np.uint64(1) << (ids % 64).astype(np.uint64))
+    inv = np.unpackbits(bits.view(np.uint8), axis=1).sum(1)
+    wf = (inv + rng.integers(0, 200, n)).astype(np.uint32)
+    ln = rng.integers(0, 60000, n).astype(np.int32)
+    bits[::17] = 0
+    wf[::17] = 0
+    ln[::17] = 0
+    cc = (rng.random(n) < 0.3).astype(np.uint8)
+    return FileBatch(bits, wf, ln, cc)
+
+
+def test_files_resembling_nothing(config3, monkeypatch):
+    c, _ = config3
+    fb = _random_files(c, 1500, seed=3, density=0.05)
+    _check(c, fb, monkeypatch)
+
+
+def test_slow_envelope_files(config3, monkeypatch):
+    c, fb = config3
+    from licensee_amd._native import FileBatch
+    part = FileBatch(fb.bits[:4000], fb.wordset_size[:4000], fb.length[:4000], fb.cc_false_positive[:4000])
+    wide, idx = widen_lanes(part, seed=11)
+    assert idx.size > 100
+    _check(c, wide, monkeypatch)
+
+
+def test_duplicate_templates_tie_to_the_later_key(config3, monkeypatch):
+    """Templates 0..99 of the config-3 corpus, then each of the first 40 again: every file
+    derived from a duplicated template ties exactly with its copy, and the later index wins."""
+    from licensee_amd.synth import SyntheticCorpus
+    c3, _ = config3
+    base = ArrayCorpus.of(c3)
+    sel = np.r_[np.arange(100), np.arange(40)]
+    c = ArrayCorpus(base.lf_bits[sel], base.lf_size[sel], base.fields_set_size[sel], base.length_slack[sel],
+                    base.length[sel], base.is_cc[sel], base.n_vocab)
+    fb = SyntheticCorpus(c3).generate(0, 6000, seed=5, nthreads=16)
+    res = _check(c, fb, monkeypatch, thresholds=(0.0,))
+    best = res[0.0][0]
+    assert np.all((best < 0) | (best >= 40))   # templates 0..39 always lose the tie to 100..139
+    assert np.any(best >= 100)
+
+
+def test_tiny_vocabulary(monkeypatch):
+    """T = 100 random templates over 60 words (one u64 word: one word per lane at most)."""
+    rng = np.random.default_rng(9)
+    T, V = 100, 60
+    bits = np.zeros((T, 1), np.uint64)
+    for t in range(T):
+        ids = np.nonzero(rng.random(V) < rng.uniform(0.05, 0.6))[0]
+        bits[t, 0] = np.bitwise_or.reduce(np.uint64(1) << ids.astype(np.uint64)) if ids.size else 0
+    lf = np.unpackbits(bits.view(np.uint8), axis=1).sum(1).astype(np.uint32)
+    fields = np.minimum(lf, rng.integers(0, 3, T)).astype(np.uint32)
+    c = ArrayCorpus(bits, lf, fields, rng.integers(-1, 40, T), rng.integers(50, 2000, T),
+                    (rng.random(T) < 0.1).astype(np.uint8), V)
+    fb = _random_files(c, 3000, seed=10, density=0.6)
+    _check(c, fb, monkeypatch)
+
+
+def test_t700(monkeypatch):
+    """T = 700: 11 templates per lane (the last lane round partly empty)."""
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from licensee_amd.synth import SyntheticCorpus
+    from licensee_amd.synth_templates import synthetic_templates
+    c = TemplateCorpus(synthetic_templates(License.all(hidden=True, pseudo=False), 700, seed=700))
+    fb = SyntheticCorpus(c).generate(0, 5000, seed=701, nthreads=16)
+    _check(c, fb, monkeypatch)
+    _check(c, _random_files(c, 500, seed=702, density=0.03), monkeypatch, thresholds=(0.0,))
