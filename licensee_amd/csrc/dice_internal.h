@@ -65,8 +65,9 @@ struct dice_ctx {
     void* d_qa = nullptr;      // [T][kPruneGroups / 2] u32: |Lf ∩ group g| as u16 pairs
     void* d_qoff = nullptr;    // [T + 1] u32 record offsets
     void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
+    void* d_qtc = nullptr;     // [padded T] uint4 template constants (dice_prune.hip)
     bool prune = false;
-    int32_t prune_sched = 0;
+    int32_t prune_sched = 0, prune_groups = 16, n_cu = 256;
     int64_t prune_records = 0;
 };
 

@@ -38,7 +38,6 @@
 namespace dice {
 
 constexpr int kPruneWaves = 16;          // waves per workgroup
-constexpr int kPruneFPW = 4;             // files per wave
 constexpr int kPruneGroups = 16;         // word groups of the bound (u16 pairs: 8 dwords per template)
 constexpr int kPruneMaxJ = 8;            // u64 words per lane: w64 <= 512 (V <= 32768)
 constexpr int kPruneMaxT = 704;          // = kPostMaxTpad (the key's low 10 bits hold the template)
@@ -75,42 +74,49 @@ __device__ __forceinline__ void prune_load(PruneNext<J>& nx, const uint64_t* __r
     nx.cc = ccp[file];
 }
 
-// f32 upper bound of (m * 200.0) / den rounded up to the key grid (low 10 bits = template).
-// The relative error of the f32 evaluation (conversions, v_rcp_f32, two products) is < 2^-20;
-// the 1 + 2^-16 factor covers it, and the key rounding only raises the value further.
-__device__ __forceinline__ uint32_t bound_key(uint32_t m, int32_t den, int32_t t) {
-    if (den <= 0) return 0x7F800000u | (uint32_t)t;   // +inf: never dropped
-    const float fb = (float)m * 200.0f * __builtin_amdgcn_rcpf((float)den) * 1.0000153f;
-    const uint32_t kb = max((__float_as_uint(fb) + kKeyLow) & ~kKeyLow, kKeyLow + 1);
-    return kb | (uint32_t)t;
+// Key of a template: an f32 upper bound of (m * 200.0) / den rounded UP to the key grid, the
+// template index + 1 in the low 10 bits (0 = no template). The relative error of the f32
+// evaluation (conversions, v_rcp_f32, two products) is < 2^-20; the 1 + 2^-16 factor covers
+// it. den == 0 gives +inf or NaN: never dropped (den < 0 cannot occur, see below).
+__device__ __forceinline__ uint32_t bound_key(uint32_t m, int32_t den, uint32_t tp1) {
+    const float fb = (float)m * (200.0f * 1.0000153f) * __builtin_amdgcn_rcpf((float)den);
+    return ((__float_as_uint(fb) + kKeyLow) & ~kKeyLow) | tp1;
 }
 
-template <int J, int TJ, int NW, bool PF, int OCC>
+// Per-template constants in LDS (uint4), padded to TJ * 64 templates:
+//   x = length, y = -max(slack, 0) (u32), z = base = |Lf| - |Fld|,
+//   w = keep bits (bit 0: kept for unflagged files, bit 1: for CC-flagged files; 0 = padding)
+//       | slack << 16 (int16, -1 = simple delta)
+// max(|len - len_F| - max(slack, 0), 0) equals the reference's adjusted delta for slack >= 0
+// and the plain delta for slack = -1 (content_helper.rb:337-347; dice_den).
+template <int J, int TJ, int G, int NW, bool PF, int OCC>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void dice_prune_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint32_t* __restrict__ qa,
-    const uint2* __restrict__ tc, const uint32_t* __restrict__ qoff, const uint4* __restrict__ qrec,
+    const uint4* __restrict__ tc, const uint32_t* __restrict__ qoff, const uint4* __restrict__ qrec,
     const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
     int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast) {
-    // LDS: [waves][w64] file rows | [T][8] group counts | [T] packed constants | [T + 1] record offsets
+    constexpr int kTP = TJ * kWave;   // padded template count
+    constexpr int kGW = G / 2;        // group-count dwords per template
+    // LDS: [waves][w64] file rows | [kTP][kGW] group counts | [kTP] constants | [T + 1] record offsets
     extern __shared__ uint64_t lds[];
     uint32_t* sqa = reinterpret_cast<uint32_t*>(lds + (size_t)NW * w64);
-    uint2* stc = reinterpret_cast<uint2*>(sqa + (size_t)T * (kPruneGroups / 2));
-    uint32_t* soff = reinterpret_cast<uint32_t*>(stc + T);
+    uint4* stc = reinterpret_cast<uint4*>(sqa + (size_t)kTP * kGW);
+    uint32_t* soff = reinterpret_cast<uint32_t*>(stc + kTP);
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     uint64_t* myrow = lds + (size_t)wave * w64;
-    for (int i = threadIdx.x; i < T * (kPruneGroups / 2); i += NW * kWave) sqa[i] = qa[i];
-    for (int i = threadIdx.x; i < T; i += NW * kWave) stc[i] = tc[i];
+    for (int i = threadIdx.x; i < kTP * kGW; i += NW * kWave) sqa[i] = qa[i];
+    for (int i = threadIdx.x; i < kTP; i += NW * kWave) stc[i] = tc[i];
     for (int i = threadIdx.x; i <= T; i += NW * kWave) soff[i] = qoff[i];
 
-    const int64_t f0 = (int64_t)blockIdx.x * (NW * kPruneFPW) + wave;
+    // files: wave-strided over the grid (persistent: ~2 workgroups per CU, tables loaded once)
+    const int64_t f0 = (int64_t)blockIdx.x * NW + wave;
+    const int64_t fstride = (int64_t)gridDim.x * NW;
     PruneNext<J> nx;
     if (PF && f0 < n) prune_load<J>(nx, rows, f0, w64, wfp, lenp, ccp, lane);
     __syncthreads();
 
-    for (int i = 0; i < kPruneFPW; ++i) {
-        const int64_t file = f0 + (int64_t)i * NW;
-        if (file >= n) break;   // wave-uniform
+    for (int64_t file = f0; file < n; file += fstride) {   // wave-uniform
         if (!PF) prune_load<J>(nx, rows, file, w64, wfp, lenp, ccp, lane);
         // the file's row into the wave's LDS row; per-lane bit counts
         uint32_t pc = 0;
@@ -122,43 +128,43 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         }
         const uint32_t wf = nx.wf;
         const int32_t lf = nx.lf;
-        const bool ccf = nx.cc != 0;
-        if (PF && i + 1 < kPruneFPW && file + NW < n)
-            prune_load<J>(nx, rows, file + NW, w64, wfp, lenp, ccp, lane);
-        // group g = lane / 4: 4-lane sums (DPP quad_perm), packed two groups per dword
+        const uint32_t ccf = nx.cc != 0 ? 1u : 0u;
+        if (PF && file + fstride < n) prune_load<J>(nx, rows, file + fstride, w64, wfp, lenp, ccp, lane);
+        // group g = lane / (64 / G): sums over 4 (8) lanes, two groups per dword
         pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
         pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-        uint32_t fg[kPruneGroups / 2];
+        if (G == 8) pc += (uint32_t)__builtin_amdgcn_ds_swizzle((int)pc, 0x101F);   // lane ^ 4
+        uint32_t fg[kGW];
 #pragma unroll
-        for (int k = 0; k < kPruneGroups / 2; ++k)
-            fg[k] = rfl(__builtin_amdgcn_readlane(pc, 8 * k) | (__builtin_amdgcn_readlane(pc, 8 * k + 4) << 16));
+        for (int k = 0; k < kGW; ++k)
+            fg[k] = rfl(__builtin_amdgcn_readlane(pc, 2 * k * (64 / G)) |
+                        (__builtin_amdgcn_readlane(pc, (2 * k + 1) * (64 / G)) << 16));
+        // a file outside the plain range (len_F < 0, |W_F| >= 2^30: never from real text) keeps
+        // every template: all are scored exactly (int32 den stays as dice_den computes it)
+        const bool plain = lf >= 0 && wf < (1u << 30);
 
-        // bounds of every unmasked template (lanes = templates t = lane + 64 j)
+        // bounds (lanes = templates t = lane + 64 j), branch-free over the padded table
         uint32_t key[TJ];
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
             const int32_t t = lane + j * kWave;
-            key[j] = 0;
-            if (t < T) {
-                const uint2 c = stc[t];   // {len | cc << 31, base | slack << 16}
-                if (!((c.x >> 31) && ccf)) {
-                    const uint4 a0 = *reinterpret_cast<const uint4*>(sqa + (size_t)t * 8);
-                    const uint4 a1 = *reinterpret_cast<const uint4*>(sqa + (size_t)t * 8 + 4);
-                    uint32_t acc = 0;
-                    acc = pk_min_add(acc, a0.x, fg[0]);
-                    acc = pk_min_add(acc, a0.y, fg[1]);
-                    acc = pk_min_add(acc, a0.z, fg[2]);
-                    acc = pk_min_add(acc, a0.w, fg[3]);
-                    acc = pk_min_add(acc, a1.x, fg[4]);
-                    acc = pk_min_add(acc, a1.y, fg[5]);
-                    acc = pk_min_add(acc, a1.z, fg[6]);
-                    acc = pk_min_add(acc, a1.w, fg[7]);
-                    const uint32_t m = (acc & 0xFFFFu) + (acc >> 16);
-                    const int32_t den = dice_den(make_int4((int32_t)(c.y & 0xFFFFu), (int32_t)c.y >> 16,
-                                                           (int32_t)(c.x & 0x7FFFFFFFu), 0), wf, lf);
-                    key[j] = bound_key(m, den, t);
-                }
+            const uint4 c = stc[t];
+            const uint32_t* a = sqa + (size_t)t * kGW;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int q = 0; q < kGW; q += 4) {
+                const uint4 a4 = *reinterpret_cast<const uint4*>(a + q);
+                acc = pk_min_add(acc, a4.x, fg[q]);
+                acc = pk_min_add(acc, a4.y, fg[q + 1]);
+                acc = pk_min_add(acc, a4.z, fg[q + 2]);
+                acc = pk_min_add(acc, a4.w, fg[q + 3]);
             }
+            const uint32_t m = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, acc), (u16x2){1, 1}, 0u, false);
+            const int32_t adj = max((int32_t)__usad(c.x, (uint32_t)lf, c.y), 0);
+            const int32_t den = (int32_t)(c.z + wf + ((uint32_t)adj >> 2));
+            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)c.w, ccf, 1);   // 0 or ~0
+            const uint32_t tp1 = (uint32_t)t + 1u;
+            key[j] = keep & (plain ? bound_key(m, den, tp1) : (0x7F800000u | tp1));
         }
         // the file's row is read by other lanes below: LDS ops of a wave run in order
         __builtin_amdgcn_wave_barrier();
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
             }
             const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
             if (K == 0) break;   // every template scored or dropped
-            const int32_t ts = (int32_t)(K & kKeyLow);
+            const int32_t ts = (int32_t)(K & kKeyLow) - 1;
             if (lane == (ts & (kWave - 1))) {
 #pragma unroll
                 for (int j = 0; j < TJ; ++j)
@@ -193,9 +199,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
                 acc += (uint32_t)__builtin_popcount((uint32_t)fb & b.y) + (uint32_t)__builtin_popcount((uint32_t)(fb >> 32) & b.z);
             }
             const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
-            const uint2 c = stc[ts];
-            const int32_t den = dice_den(make_int4((int32_t)(c.y & 0xFFFFu), (int32_t)c.y >> 16,
-                                                   (int32_t)(c.x & 0x7FFFFFFFu), 0), wf, lf);
+            const uint4 c = stc[ts];
+            const int32_t den = dice_den(make_int4((int32_t)c.z, (int32_t)c.w >> 16, (int32_t)c.x, 0), wf, lf);
             const bool better = fast ? outranks_t<true>(ts, ov, den, bi, bo, bd) : outranks_t<false>(ts, ov, den, bi, bo, bd);
             if (better) {
                 bi = ts;
@@ -218,76 +223,99 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
 
 // ---- host side ---------------------------------------------------------------------------
 
-static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
-    return (size_t)nw * w64 * 8 + (size_t)T * (kPruneGroups / 2) * 4 + (size_t)T * 8 + ((size_t)T + 1) * 4;
+static int32_t prune_tj(int32_t T) { return T <= 640 ? 10 : (kPruneMaxT + kWave - 1) / kWave; }
+
+static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T, int32_t groups) {
+    const size_t tp = (size_t)prune_tj(T) * kWave;
+    return (size_t)nw * w64 * 8 + tp * (groups / 2) * 4 + tp * 16 + ((size_t)T + 1) * 4;
 }
 
 int prune_setup(dice_ctx* c, const dice_templates* t) {
     const char* e = getenv("DICE_POST_PRUNE");
     if (e && *e == '0') return DICE_OK;
+    const char* eg = getenv("DICE_PRUNE_GROUPS");
+    const int32_t G = eg && *eg && atoi(eg) == 8 ? 8 : kPruneGroups;
     const int32_t T = c->T, w64 = c->w64;
-    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024) return DICE_OK;
-    // group counts |Lf_t ∩ g| (< 2^16: post_feasible bounds |Lf|), records of nonzero u64 words
-    std::vector<uint32_t> qa((size_t)T * (kPruneGroups / 2), 0);
+    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T, G) > 160 * 1024)
+        return DICE_OK;
+    const size_t tp = (size_t)prune_tj(T) * kWave;
+    // group counts |Lf_t ∩ g| (< 2^16: post_feasible bounds |Lf|) as u16 pairs, the constants,
+    // records of the nonzero u64 words; padding templates have keep bits 0
+    std::vector<uint32_t> qa(tp * (G / 2), 0);
+    std::vector<uint4> tcv(tp, make_uint4(0, 0, 0, 0));
     std::vector<uint32_t> qoff((size_t)T + 1, 0);
     std::vector<uint4> qrec;
     for (int32_t i = 0; i < T; ++i) {
         const uint64_t* r = t->lf_bits + (size_t)i * w64;
-        uint32_t g16[kPruneGroups] = {0};
+        uint32_t gc[kPruneGroups] = {0};
         for (int32_t p = 0; p < w64; ++p) {
             if (!r[p]) continue;
-            g16[(p % kWave) / 4] += (uint32_t)__builtin_popcountll(r[p]);
+            gc[(p % kWave) / (kWave / G)] += (uint32_t)__builtin_popcountll(r[p]);
             qrec.push_back(make_uint4((uint32_t)p, (uint32_t)r[p], (uint32_t)(r[p] >> 32), 0));
         }
-        for (int k = 0; k < kPruneGroups / 2; ++k) qa[(size_t)i * 8 + k] = g16[2 * k] | (g16[2 * k + 1] << 16);
+        for (int k = 0; k < G / 2; ++k) qa[(size_t)i * (G / 2) + k] = gc[2 * k] | (gc[2 * k + 1] << 16);
         qoff[(size_t)i + 1] = (uint32_t)qrec.size();
+        const int32_t slack = t->length_slack[i];
+        tcv[(size_t)i] = make_uint4((uint32_t)t->length[i], (uint32_t)(-std::max(slack, 0)),
+                                    t->lf_size[i] - t->fields_set_size[i],
+                                    (t->is_cc[i] ? 1u : 3u) | ((uint32_t)(slack & 0xFFFF) << 16));
     }
     if (qrec.empty()) qrec.push_back(make_uint4(0, 0, 0, 0));
     int rc;
     if ((rc = dalloc_bytes(&c->d_qa, qa.size() * 4)) || (rc = dalloc_bytes(&c->d_qoff, qoff.size() * 4)) ||
-        (rc = dalloc_bytes(&c->d_qrec, qrec.size() * sizeof(uint4))))
+        (rc = dalloc_bytes(&c->d_qrec, qrec.size() * sizeof(uint4))) ||
+        (rc = dalloc_bytes(&c->d_qtc, tcv.size() * sizeof(uint4))))
         return rc;
     if (hipMemcpy(c->d_qa, qa.data(), qa.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_qoff, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_qrec, qrec.data(), qrec.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(c->d_qrec, qrec.data(), qrec.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_qtc, tcv.data(), tcv.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "pruned-match plan upload failed");
     c->prune_records = (int64_t)qoff[(size_t)T];
     const char* sc = getenv("DICE_PRUNE_SCHED");
     c->prune_sched = sc && *sc ? atoi(sc) : 0;
+    c->prune_groups = G;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
+        c->n_cu = 256;
     c->prune = true;
     return DICE_OK;
 }
 
-template <int J, int TJ, int NW, bool PF, int OCC>
+template <int J, int TJ, int G, int NW, bool PF, int OCC>
 static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
-    auto kern = dice_prune_match<J, TJ, NW, PF, OCC>;
+    const size_t lds = prune_lds_bytes(NW, c->w64, c->T, G);
+    auto kern = dice_prune_match<J, TJ, G, NW, PF, OCC>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
-    const int64_t groups = (b->n + NW * kPruneFPW - 1) / (NW * kPruneFPW);
+    // persistent grid: as many workgroups as are resident at once (LDS- and wave-limited)
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / NW, (160 * 1024) / (int64_t)lds));
+    const int64_t groups = std::min<int64_t>((b->n + NW - 1) / NW, per_cu * c->n_cu);
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows,
-                       b->n, c->w64, c->T, (const uint32_t*)c->d_qa, (const uint2*)c->d_ptc,
+                       b->n, c->w64, c->T, (const uint32_t*)c->d_qa, (const uint4*)c->d_qtc,
                        (const uint32_t*)c->d_qoff, (const uint4*)c->d_qrec, b->d_wf, b->d_len, b->d_cc, thr,
                        b->d_best, b->d_ov, b->d_score, c->post_fast);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
 }
 
 // Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, row loads at the file;
-// 1 = 8-wave workgroups, the next file's row prefetched in VGPRs (6 waves/SIMD);
-// 2 = 8-wave workgroups, row loads at the file (8 waves/SIMD).
-template <int J, int TJ>
+// 1 = 16-wave workgroups, the next file's row prefetched in VGPRs; 2 = 8-wave workgroups,
+// the next row prefetched (6 waves/SIMD); 3 = 8-wave workgroups, row loads at the file.
+template <int J, int TJ, int G>
 static int launch_prune_s(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     switch (c->prune_sched) {
-        case 1: return launch_prune<J, TJ, 8, true, 6>(c, b, thr, s);
-        case 2: return launch_prune<J, TJ, 8, false, 8>(c, b, thr, s);
-        default: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
+        case 1: return launch_prune<J, TJ, G, 16, true, 8>(c, b, thr, s);
+        case 2: return launch_prune<J, TJ, G, 8, true, 6>(c, b, thr, s);
+        case 3: return launch_prune<J, TJ, G, 8, false, 8>(c, b, thr, s);
+        default: return launch_prune<J, TJ, G, 16, false, 8>(c, b, thr, s);
     }
 }
 
 template <int J>
 static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    return c->T <= 640 ? launch_prune_s<J, 10>(c, b, thr, s)
-                       : launch_prune_s<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
+    constexpr int kTJ11 = (kPruneMaxT + kWave - 1) / kWave;
+    if (c->prune_groups == 8)
+        return c->T <= 640 ? launch_prune_s<J, 10, 8>(c, b, thr, s) : launch_prune_s<J, kTJ11, 8>(c, b, thr, s);
+    return c->T <= 640 ? launch_prune_s<J, 10, 16>(c, b, thr, s) : launch_prune_s<J, kTJ11, 16>(c, b, thr, s);
 }
 
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
