@@ -67,7 +67,7 @@ struct dice_ctx {
     void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
     void* d_qtc = nullptr;     // [padded T] uint4 template constants (dice_prune.hip)
     bool prune = false;
-    int32_t prune_sched = 0, prune_groups = 16, n_cu = 256;
+    int32_t prune_sched = 0, prune_groups = 16, n_cu = 256, prune_diag = 0;
     int64_t prune_records = 0;
 };
 

@@ -45,9 +45,12 @@ constexpr uint32_t kKeyLow = 1023u;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t pk_min_add(uint32_t acc, uint32_t a, uint32_t f) {
-    const u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, f));
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, acc) + m);
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
 
 // The next file's independent loads, in flight while the wave works on the current file.
@@ -83,6 +86,37 @@ __device__ __forceinline__ uint32_t bound_key(uint32_t m, int32_t den, uint32_t 
     return ((__float_as_uint(fb) + kKeyLow) & ~kKeyLow) | tp1;
 }
 
+// Exact overlap of template ts with the wave's file row (one lane per record {u64 word, mask},
+// two records per lane in flight), its denominator and the running best in the strict
+// (score, later key) order; llo becomes an f32 lower bound of the best score.
+__device__ __forceinline__ void score_template(int32_t ts, const uint32_t* soff, const uint4* __restrict__ qrec,
+                                               const uint64_t* myrow, const uint4* stc, uint32_t wf, int32_t lf,
+                                               bool fast, int lane, int32_t& bi, uint32_t& bo, int32_t& bd,
+                                               float& llo) {
+    const uint32_t r0 = rfl(soff[ts]), r1 = rfl(soff[ts + 1]);
+    uint32_t acc = 0;
+    for (uint32_t r = r0 + lane; r < r1; r += 2 * kWave) {
+        const uint4 a = qrec[r];
+        const uint4 b = r + kWave < r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+        const uint64_t fa = myrow[a.x], fb = myrow[b.x];
+        acc += (uint32_t)__builtin_popcount((uint32_t)fa & a.y) + (uint32_t)__builtin_popcount((uint32_t)(fa >> 32) & a.z);
+        acc += (uint32_t)__builtin_popcount((uint32_t)fb & b.y) + (uint32_t)__builtin_popcount((uint32_t)(fb >> 32) & b.z);
+    }
+    const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
+    const uint4 c = stc[ts];
+    const int32_t den = dice_den(make_int4((int32_t)c.z, (int32_t)c.w >> 16, (int32_t)c.x, 0), wf, lf);
+    const bool better = fast ? outranks_t<true>(ts, ov, den, bi, bo, bd) : outranks_t<false>(ts, ov, den, bi, bo, bd);
+    if (better) {
+        bi = ts;
+        bo = ov;
+        bd = den;
+        const double s = dice_score(bo, bd);
+        // f32 lower bound of s: (1 - 2^-16) s rounds to nearest below s; no dropping against a
+        // non-positive or NaN best
+        llo = s > 0.0 ? (float)(s * (1.0 - 1.0 / 65536.0)) : -1.0f;
+    }
+}
+
 // Per-template constants in LDS (uint4), padded to TJ * 64 templates:
 //   x = length, y = -max(slack, 0) (u32), z = base = |Lf| - |Fld|,
 //   w = keep bits (bit 0: kept for unflagged files, bit 1: for CC-flagged files; 0 = padding)
@@ -94,12 +128,16 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint32_t* __restrict__ qa,
     const uint4* __restrict__ tc, const uint32_t* __restrict__ qoff, const uint4* __restrict__ qrec,
     const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
-    int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast) {
+    int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast, int32_t diag) {
+    // diag (DICE_PRUNE_DIAG, diagnostics only -- results are wrong): 1 skips the bound pass (one
+    // template scored), 2 skips exact scoring, 4 skips the row loads
     constexpr int kTP = TJ * kWave;   // padded template count
     constexpr int kGW = G / 2;        // group-count dwords per template
-    // LDS: [waves][w64] file rows | [kTP][kGW] group counts | [kTP] constants | [T + 1] record offsets
+    // LDS: [waves][w64] file rows | [kGW / 4][kTP] uint4 group counts (lane stride 16 B: no bank
+    // conflicts) | [kTP] constants | [T + 1] record offsets
     extern __shared__ uint64_t lds[];
     uint32_t* sqa = reinterpret_cast<uint32_t*>(lds + (size_t)NW * w64);
+    const uint4* sqa4 = reinterpret_cast<const uint4*>(sqa);
     uint4* stc = reinterpret_cast<uint4*>(sqa + (size_t)kTP * kGW);
     uint32_t* soff = reinterpret_cast<uint32_t*>(stc + kTP);
     const int lane = threadIdx.x & (kWave - 1);
@@ -117,7 +155,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
     __syncthreads();
 
     for (int64_t file = f0; file < n; file += fstride) {   // wave-uniform
-        if (!PF) prune_load<J>(nx, rows, file, w64, wfp, lenp, ccp, lane);
+        if (!PF) prune_load<J>(nx, rows, (diag & 4) ? (file & 63) : file, w64, wfp, lenp, ccp, lane);
         // the file's row into the wave's LDS row; per-lane bit counts
         uint32_t pc = 0;
 #pragma unroll
@@ -143,28 +181,37 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         // every template: all are scored exactly (int32 den stays as dice_den computes it)
         const bool plain = lf >= 0 && wf < (1u << 30);
 
-        // bounds (lanes = templates t = lane + 64 j), branch-free over the padded table
+        // bounds (lanes = templates t = lane + 64 j), branch-free over the padded table; each
+        // lane keeps its two largest keys
         uint32_t key[TJ];
+        uint32_t m1 = 0, m2 = 0;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
+            if (diag & 1) { key[j] = (j == 0 && lane == 0) ? 0x7F800001u : 0u; m1 = max(m1, key[j]); continue; }
             const int32_t t = lane + j * kWave;
             const uint4 c = stc[t];
-            const uint32_t* a = sqa + (size_t)t * kGW;
-            uint32_t acc = 0;
+            uint32_t mn[kGW];
 #pragma unroll
             for (int q = 0; q < kGW; q += 4) {
-                const uint4 a4 = *reinterpret_cast<const uint4*>(a + q);
-                acc = pk_min_add(acc, a4.x, fg[q]);
-                acc = pk_min_add(acc, a4.y, fg[q + 1]);
-                acc = pk_min_add(acc, a4.z, fg[q + 2]);
-                acc = pk_min_add(acc, a4.w, fg[q + 3]);
+                const uint4 a4 = sqa4[(q / 4) * kTP + t];
+                mn[q] = pk_min(a4.x, fg[q]);
+                mn[q + 1] = pk_min(a4.y, fg[q + 1]);
+                mn[q + 2] = pk_min(a4.z, fg[q + 2]);
+                mn[q + 3] = pk_min(a4.w, fg[q + 3]);
             }
-            const uint32_t m = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, acc), (u16x2){1, 1}, 0u, false);
+#pragma unroll
+            for (int h = kGW / 2; h >= 1; h /= 2)   // pairwise u16 sums (short dependency chains)
+#pragma unroll
+                for (int q = 0; q < h; ++q) mn[q] = pk_add(mn[q], mn[q + h]);
+            const uint32_t m = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, mn[0]), (u16x2){1, 1}, 0u, false);
             const int32_t adj = max((int32_t)__usad(c.x, (uint32_t)lf, c.y), 0);
             const int32_t den = (int32_t)(c.z + wf + ((uint32_t)adj >> 2));
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)c.w, ccf, 1);   // 0 or ~0
             const uint32_t tp1 = (uint32_t)t + 1u;
-            key[j] = keep & (plain ? bound_key(m, den, tp1) : (0x7F800000u | tp1));
+            const uint32_t k = keep & (plain ? bound_key(m, den, tp1) : (0x7F800000u | tp1));
+            key[j] = k;
+            m2 = max(m2, min(m1, k));
+            m1 = max(m1, k);
         }
         // the file's row is read by other lanes below: LDS ops of a wave run in order
         __builtin_amdgcn_wave_barrier();
@@ -173,43 +220,39 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         int32_t bi = -1, bd = 1;
         uint32_t bo = 0;
         float llo = -1.0f;   // lower bound of the best score (f32); bounds below it are dropped
-        for (;;) {
-            uint32_t km = 0;
+        // the largest key, scored first, and the second largest (keys are distinct): if the
+        // second is below the first template's score, so is every other and the file is done
+        const uint32_t K1 = rfl(__builtin_amdgcn_readlane(wave_incl_max(m1), kWave - 1));
+        if (K1 != 0) {
+            const uint32_t K2 = rfl(__builtin_amdgcn_readlane(wave_incl_max(m1 == K1 ? m2 : m1), kWave - 1));
+            if (diag & 2) { bi = (int32_t)(K1 & kKeyLow) - 1; bo = K2; } else
+            score_template((int32_t)(K1 & kKeyLow) - 1, soff, qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
+            if (!(diag & 2) && K2 != 0 && !(__uint_as_float(K2 & ~kKeyLow) < llo)) {
+                // more templates may reach the top: drop the scored one, then score the largest
+                // remaining key and drop every key below the best score, until none is left
+                const int32_t t1 = (int32_t)(K1 & kKeyLow) - 1;
+                if (lane == (t1 & (kWave - 1))) {
 #pragma unroll
-            for (int j = 0; j < TJ; ++j) {
-                if (__uint_as_float(key[j] & ~kKeyLow) < llo) key[j] = 0;
-                km = max(km, key[j]);
-            }
-            const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
-            if (K == 0) break;   // every template scored or dropped
-            const int32_t ts = (int32_t)(K & kKeyLow) - 1;
-            if (lane == (ts & (kWave - 1))) {
+                    for (int j = 0; j < TJ; ++j)
+                        if (j == (t1 >> 6)) key[j] = 0;
+                }
+                for (;;) {
+                    uint32_t km = 0;
 #pragma unroll
-                for (int j = 0; j < TJ; ++j)
-                    if (j == (ts >> 6)) key[j] = 0;
-            }
-            // exact overlap: one lane per record of template ts, two records per lane in flight
-            const uint32_t r0 = rfl(soff[ts]), r1 = rfl(soff[ts + 1]);
-            uint32_t acc = 0;
-            for (uint32_t r = r0 + lane; r < r1; r += 2 * kWave) {
-                const uint4 a = qrec[r];
-                const uint4 b = r + kWave < r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
-                const uint64_t fa = myrow[a.x], fb = myrow[b.x];
-                acc += (uint32_t)__builtin_popcount((uint32_t)fa & a.y) + (uint32_t)__builtin_popcount((uint32_t)(fa >> 32) & a.z);
-                acc += (uint32_t)__builtin_popcount((uint32_t)fb & b.y) + (uint32_t)__builtin_popcount((uint32_t)(fb >> 32) & b.z);
-            }
-            const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
-            const uint4 c = stc[ts];
-            const int32_t den = dice_den(make_int4((int32_t)c.z, (int32_t)c.w >> 16, (int32_t)c.x, 0), wf, lf);
-            const bool better = fast ? outranks_t<true>(ts, ov, den, bi, bo, bd) : outranks_t<false>(ts, ov, den, bi, bo, bd);
-            if (better) {
-                bi = ts;
-                bo = ov;
-                bd = den;
-                const double s = dice_score(bo, bd);
-                // f32 lower bound of s: (1 - 2^-16) s rounds to nearest below s; no dropping
-                // against a non-positive or NaN best
-                llo = s > 0.0 ? (float)(s * (1.0 - 1.0 / 65536.0)) : -1.0f;
+                    for (int j = 0; j < TJ; ++j) {
+                        if (__uint_as_float(key[j] & ~kKeyLow) < llo) key[j] = 0;
+                        km = max(km, key[j]);
+                    }
+                    const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
+                    if (K == 0) break;   // every template scored or dropped
+                    const int32_t ts = (int32_t)(K & kKeyLow) - 1;
+                    if (lane == (ts & (kWave - 1))) {
+#pragma unroll
+                        for (int j = 0; j < TJ; ++j)
+                            if (j == (ts >> 6)) key[j] = 0;
+                    }
+                    score_template(ts, soff, qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
+                }
             }
         }
         if (lane == 0) {
@@ -253,7 +296,8 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
             gc[(p % kWave) / (kWave / G)] += (uint32_t)__builtin_popcountll(r[p]);
             qrec.push_back(make_uint4((uint32_t)p, (uint32_t)r[p], (uint32_t)(r[p] >> 32), 0));
         }
-        for (int k = 0; k < G / 2; ++k) qa[(size_t)i * (G / 2) + k] = gc[2 * k] | (gc[2 * k + 1] << 16);
+        for (int k = 0; k < G / 2; ++k)   // [G / 8][tp] uint4 planes
+            qa[((size_t)(k / 4) * tp + (size_t)i) * 4 + (k % 4)] = gc[2 * k] | (gc[2 * k + 1] << 16);
         qoff[(size_t)i + 1] = (uint32_t)qrec.size();
         const int32_t slack = t->length_slack[i];
         tcv[(size_t)i] = make_uint4((uint32_t)t->length[i], (uint32_t)(-std::max(slack, 0)),
@@ -275,6 +319,8 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     const char* sc = getenv("DICE_PRUNE_SCHED");
     c->prune_sched = sc && *sc ? atoi(sc) : 0;
     c->prune_groups = G;
+    const char* dg = getenv("DICE_PRUNE_DIAG");
+    c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
         c->n_cu = 256;
     c->prune = true;
@@ -293,7 +339,7 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows,
                        b->n, c->w64, c->T, (const uint32_t*)c->d_qa, (const uint4*)c->d_qtc,
                        (const uint32_t*)c->d_qoff, (const uint4*)c->d_qrec, b->d_wf, b->d_len, b->d_cc, thr,
-                       b->d_best, b->d_ov, b->d_score, c->post_fast);
+                       b->d_best, b->d_ov, b->d_score, c->post_fast, c->prune_diag);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
 }
 
