@@ -19,9 +19,11 @@ The JSON line also carries:
   cpu_baseline -- oracle/dice_ref.c (C port of the reference Set#& algorithm), rank 0 at N=1,
                   on a bounded sample of the same files, on every core the process may use.
   parity       -- GPU results of the timed run vs the C oracle's hash mode on that sample.
-  extras.configs -- at N=1, the other BASELINE configs (3: ~600 templates, LDS kernel; 4:
-                  long/mixed files; 5: full matrix + top-k) measured in the same run, each with
-                  its own HIP-event launch time, roofline fraction and oracle parity sample.
+  extras.configs -- at N=1, the other BASELINE configs (3: ~600 templates, bound-pruned match
+                  kernel, plus '3-allpairs': the same files on the postings kernel, which scores
+                  every pair; 4: long/mixed files; 5: full matrix + top-k) measured in the same
+                  run, each with its own HIP-event launch time, roofline fraction and oracle
+                  parity sample.
 """
 from __future__ import annotations
 
@@ -39,9 +41,9 @@ sys.path.insert(0, ROOT)
 METRIC = 'license files scored/sec (whole node) vs all templates; % HBM roofline'
 HBM_PEAK_GBS = 8000.0
 DEFAULT_FILES = {2: 1_000_000, 3: 1_250_000, 4: 1_000_000, 5: 1_000_000}
-KERNELS = ['dense', 'sparse-program', 'lds-records', 'postings']
+KERNELS = ['dense', 'sparse-program', 'lds-records', 'postings', 'bound-pruned']
 WORKLOADS = {2: 'config2: synthetic perturbed LICENSE files x 47 choosealicense.com templates, Dice#match thr 98',
-             3: 'config3: synthetic files x ~600 synthetic templates (postings kernel), one GPU shard '
+             3: 'config3: synthetic files x ~600 synthetic templates, Dice#match thr 98, one GPU shard '
                 'of the 10M-file node run',
              4: 'config4: long/mixed COPYING files (2-6 templates + notices) x 47 templates',
              5: 'config5: full N x T similarity matrix + top-k x 47 templates'}
@@ -119,6 +121,7 @@ class Run:
         self.scorer = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc,
                              n_vocab=c.n_vocab, device=dev)
         self.T, self.V, self.kind, self.entries = self.scorer.info()
+        self.match_kernel = self.scorer.match_kernel() if cfg != 5 else self.kind
         self.batch = self.scorer.batch(n_per)
         out_bytes = self.T * 12 + args.topk * 12 if cfg == 5 else 16
         self.algo_bytes_per_file = self.batch.bytes_per_file() + 4 + 4 + 1 + out_bytes
@@ -134,6 +137,31 @@ class Run:
     def close(self):
         self.batch.close()
         self.scorer.close()
+
+    def rescore(self, env, dev):
+        """Swap in a scorer built under extra environment switches (read at dice_create), same
+        corpus and files; returns the old (scorer, batch) for restore()."""
+        from licensee_amd._native import Scorer
+        old_env = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            c = self.corpus
+            sc = Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc,
+                        n_vocab=c.n_vocab, device=dev)
+        finally:
+            for k, v in old_env.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        saved = (self.scorer, self.batch, self.match_kernel)
+        self.scorer, self.batch = sc, sc.batch(self.n_per)
+        self.match_kernel = sc.match_kernel()
+        return saved
+
+    def restore(self, saved):
+        self.close()
+        self.scorer, self.batch, self.match_kernel = saved
 
 
 def timed(run, steps, warmup, stream, distributed):
@@ -201,6 +229,32 @@ def parity_sample(run, orc, sptr, threads, n_sample):
     mism += int(np.sum(scm[rows, tki[sl, 0]] != tks[sl, 0]))
     return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (matrix, hash Set#&)',
             'oracle_files_per_s': sl.stop / cpu_s}
+
+
+def measure_extra(r, c, args, stream, sptr, cpu):
+    steps = min(args.steps, 20)
+    w, lm, ach = timed(r, steps, 2, stream, False)
+    tr, tr_src = traffic_for(c, r.n_per, r.T) if r.match_kernel == r.kind or c == 5 else (None, None)
+    rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'templates': r.T, 'vocab': r.V,
+           'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': r.n_per * steps / w,
+           'scores_per_s': r.n_per * steps / w * r.T, 'launch_ms': lm,
+           'algorithmic_bytes_per_file': r.algo_bytes_per_file, 'roofline_achieved_gbs': ach,
+           'roofline_frac': ach / HBM_PEAK_GBS, 'traffic': tr, 'traffic_source': tr_src}
+    if r.match_kernel == 4:
+        rec['note'] = ('bound-pruned Dice#match: every (file, template) pair is decided, but only pairs whose '
+                       'overlap bound can reach the top score are scored exactly (DESIGN.md 4); scores_per_s '
+                       'counts decided pairs. 3-allpairs scores every pair')
+    if not args.no_cpu_baseline:
+        rec['parity'] = parity_sample(r, oracle_for(r.corpus), sptr, cpu['threads'],
+                                      {3: 20_000, 4: 30_000, 5: 50_000}[c])
+        # the parity leg is the reference-equivalent CPU path on the same files: its rate
+        rec['cpu_baseline'] = {'value': rec['parity'].pop('oracle_files_per_s'), 'unit': 'files/s',
+                               'cores': cpu['threads'], 'kind': 'port',
+                               'sample': f"the parity sample: first {rec['parity']['checked_files']} files, "
+                                         f"hash-set Set#& restatement (oracle/dice_ref.c)"}
+    log(f"config {c} ({rec['kernel']}): {rec['files_per_s']:.3e} files/s, launch {lm * 1e3:.1f} us, "
+        f"frac {rec['roofline_frac']:.3f}, parity {rec.get('parity')}")
+    return rec
 
 
 def main():
@@ -372,7 +426,7 @@ def main():
             parity = parity_sample(run, orc, sptr, cpu_threads, sample)
             parity.pop('oracle_files_per_s', None)
 
-    head = {'templates': run.T, 'vocab': run.V, 'kernel': KERNELS[run.kind], 'program_entries': run.entries,
+    head = {'templates': run.T, 'vocab': run.V, 'kernel': KERNELS[run.match_kernel], 'program_entries': run.entries,
             'algorithmic_bytes_per_file': run.algo_bytes_per_file}
     # ---- the other BASELINE configs, same run (N = 1) ---------------------------------------
     if rank == 0 and world == 1 and not args.probe and args.extra_configs:
@@ -383,25 +437,14 @@ def main():
             if c == cfg:
                 continue
             r = Run(c, DEFAULT_FILES[c], 0, 1, dev, nthreads, args)
-            steps = min(args.steps, 20)
-            w, lm, ach = timed(r, steps, 2, stream, False)
-            tr, tr_src = traffic_for(c, r.n_per, r.T)
-            rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'templates': r.T, 'vocab': r.V,
-                   'kernel': KERNELS[r.kind], 'steps': steps, 'files_per_s': r.n_per * steps / w,
-                   'scores_per_s': r.n_per * steps / w * r.T, 'launch_ms': lm,
-                   'algorithmic_bytes_per_file': r.algo_bytes_per_file, 'roofline_achieved_gbs': ach,
-                   'roofline_frac': ach / HBM_PEAK_GBS, 'traffic': tr, 'traffic_source': tr_src}
-            if not args.no_cpu_baseline:
-                rec['parity'] = parity_sample(r, oracle_for(r.corpus), sptr, cpu['threads'],
-                                              {3: 20_000, 4: 30_000, 5: 50_000}[c])
-                # the parity leg is the reference-equivalent CPU path on the same files: its rate
-                rec['cpu_baseline'] = {'value': rec['parity'].pop('oracle_files_per_s'), 'unit': 'files/s',
-                                       'cores': cpu['threads'], 'kind': 'port',
-                                       'sample': f"the parity sample: first {rec['parity']['checked_files']} files, "
-                                                 f"hash-set Set#& restatement (oracle/dice_ref.c)"}
-            extras['configs'][str(c)] = rec
-            log(f"config {c}: {rec['files_per_s']:.3e} files/s, launch {lm * 1e3:.1f} us, "
-                f"frac {rec['roofline_frac']:.3f}, parity {rec.get('parity')}")
+            variants = [(str(c), None)]
+            if c == 3 and r.match_kernel == 4:
+                variants.append(('3-allpairs', {'DICE_POST_PRUNE': '0'}))
+            for tag, env in variants:
+                saved = r.rescore(env, dev) if env else None
+                extras['configs'][tag] = measure_extra(r, c, args, stream, sptr, cpu)
+                if saved:
+                    r.restore(saved)
             r.close()
 
     if rank == 0:
@@ -418,8 +461,8 @@ def main():
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'traffic_source': traffic_src,
                          'algorithmic_bytes_per_file': head['algorithmic_bytes_per_file'], 'launch_ms': launch_ms,
-                         **({'note': 'config 3 is compute-bound (VALU/LDS issue of the LDS-tiled kernel); '
-                                     'frac is its HBM share only (DESIGN.md 4b)'} if cfg == 3 else {})},
+                         **({'note': 'config 3 is latency/issue-bound, not HBM-bound; frac is its HBM share '
+                                     'only (DESIGN.md 4b)'} if cfg == 3 else {})},
             'cpu_baseline': cpu_baseline,
             'scores_per_s': value * head['templates'],
             'parity': parity,

@@ -307,7 +307,7 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
     void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc,
-                    c->d_qa, c->d_qoff, c->d_qrec, c->d_qtc};
+                    c->d_q8, c->d_qoff, c->d_qrec, c->d_qtc};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);

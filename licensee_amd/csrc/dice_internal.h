@@ -62,12 +62,12 @@ struct dice_ctx {
     bool post_fast = false;
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): per-template group counts, records
-    void* d_qa = nullptr;      // [T][kPruneGroups / 2] u32: |Lf ∩ group g| as u16 pairs
+    void* d_q8 = nullptr;      // [padded T] uint4: |Lf ∩ group g| clamped to bytes
     void* d_qoff = nullptr;    // [T + 1] u32 record offsets
     void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
     void* d_qtc = nullptr;     // [padded T] uint4 template constants (dice_prune.hip)
     bool prune = false;
-    int32_t prune_sched = 0, prune_groups = 16, n_cu = 256, prune_diag = 0;
+    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0;
     int64_t prune_records = 0;
 };
 

@@ -38,20 +38,12 @@
 namespace dice {
 
 constexpr int kPruneWaves = 16;          // waves per workgroup
-constexpr int kPruneGroups = 16;         // word groups of the bound (u16 pairs: 8 dwords per template)
+constexpr int kPruneGroups = 16;         // word groups of the bound
 constexpr int kPruneMaxJ = 8;            // u64 words per lane: w64 <= 512 (V <= 32768)
 constexpr int kPruneMaxT = 704;          // = kPostMaxTpad (the key's low 10 bits hold the template)
 constexpr uint32_t kKeyLow = 1023u;
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
-}
-
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
-}
 
 // The next file's independent loads, in flight while the wave works on the current file.
 template <int J>
@@ -104,47 +96,53 @@ __device__ __forceinline__ void score_template(int32_t ts, const uint32_t* soff,
     }
     const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
     const uint4 c = stc[ts];
-    const int32_t den = dice_den(make_int4((int32_t)c.z, (int32_t)c.w >> 16, (int32_t)c.x, 0), wf, lf);
+    const int32_t den = dice_den(make_int4((int32_t)(c.z & 0xFFFFu), (int32_t)c.w >> 16, (int32_t)c.x, 0), wf, lf);
     const bool better = fast ? outranks_t<true>(ts, ov, den, bi, bo, bd) : outranks_t<false>(ts, ov, den, bi, bo, bd);
     if (better) {
         bi = ts;
         bo = ov;
         bd = den;
-        const double s = dice_score(bo, bd);
-        // f32 lower bound of s: (1 - 2^-16) s rounds to nearest below s; no dropping against a
-        // non-positive or NaN best
-        llo = s > 0.0 ? (float)(s * (1.0 - 1.0 / 65536.0)) : -1.0f;
+        // f32 lower bound of the best score (relative error of the f32 evaluation < 2^-20, the
+        // 1 - 2^-16 factor covers it); no dropping against a best with den <= 0
+        llo = bd > 0 ? (float)bo * (200.0f * 0.99998474f) * __builtin_amdgcn_rcpf((float)bd) : -1.0f;
     }
 }
 
 // Per-template constants in LDS (uint4), padded to TJ * 64 templates:
-//   x = length, y = -max(slack, 0) (u32), z = base = |Lf| - |Fld|,
+//   x = length, y = -max(slack, 0) (u32), z = base (= |Lf| - |Fld|) | sum_g min(|Lf ∩ g|, 255) << 16,
 //   w = keep bits (bit 0: kept for unflagged files, bit 1: for CC-flagged files; 0 = padding)
 //       | slack << 16 (int16, -1 = simple delta)
 // max(|len - len_F| - max(slack, 0), 0) equals the reference's adjusted delta for slack >= 0
 // and the plain delta for slack = -1 (content_helper.rb:337-347; dice_den).
-template <int J, int TJ, int G, int NW, bool PF, int OCC>
+//
+// Group-count bound m = sum_g min(A_g, F_g) (A_g = |Lf ∩ g|, F_g = |W_F ∩ g|). When every
+// F_g <= 255 the byte-clamped A'_g = min(A_g, 255) give the same minima, and
+// min(a, f) = (a + f - |a - f|) / 2 turns the sum into one v_sad_u8 per 4 groups:
+//   m = (sum_g A'_g + sum_g F_g - sum_g |A'_g - F_g|) / 2          (16 B of table per template)
+// A file with some F_g > 255 (thousands of vocabulary words) uses the looser m = |W_F ∩ V|
+// (more templates are scored exactly; results are the same).
+template <int J, int TJ, int NW, bool PF, int OCC>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void dice_prune_match(
-    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint32_t* __restrict__ qa,
-    const uint4* __restrict__ tc, const uint32_t* __restrict__ qoff, const uint4* __restrict__ qrec,
-    const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
-    int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast, int32_t diag) {
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint4* __restrict__ q8g, const uint4* __restrict__ tc, const uint32_t* __restrict__ qoff,
+    const uint4* __restrict__ qrec, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
+    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
+    double* __restrict__ score_out, bool corpus_fast, int32_t diag) {
     // diag (DICE_PRUNE_DIAG, diagnostics only -- results are wrong): 1 skips the bound pass (one
     // template scored), 2 skips exact scoring, 4 skips the row loads
     constexpr int kTP = TJ * kWave;   // padded template count
-    constexpr int kGW = G / 2;        // group-count dwords per template
-    // LDS: [waves][w64] file rows | [kGW / 4][kTP] uint4 group counts (lane stride 16 B: no bank
-    // conflicts) | [kTP] constants | [T + 1] record offsets
+    // LDS: [waves][w64] file rows | [kTP] uint4 byte group counts | [kTP] constants | [T + 1]
+    // record offsets (lane stride 16 B: conflict-free b128 reads)
     extern __shared__ uint64_t lds[];
-    uint32_t* sqa = reinterpret_cast<uint32_t*>(lds + (size_t)NW * w64);
-    const uint4* sqa4 = reinterpret_cast<const uint4*>(sqa);
-    uint4* stc = reinterpret_cast<uint4*>(sqa + (size_t)kTP * kGW);
+    uint4* q8 = reinterpret_cast<uint4*>(lds + (size_t)NW * w64);
+    uint4* stc = q8 + kTP;
     uint32_t* soff = reinterpret_cast<uint32_t*>(stc + kTP);
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     uint64_t* myrow = lds + (size_t)wave * w64;
-    for (int i = threadIdx.x; i < kTP * kGW; i += NW * kWave) sqa[i] = qa[i];
-    for (int i = threadIdx.x; i < kTP; i += NW * kWave) stc[i] = tc[i];
+    for (int i = threadIdx.x; i < kTP; i += NW * kWave) {
+        q8[i] = q8g[i];
+        stc[i] = tc[i];
+    }
     for (int i = threadIdx.x; i <= T; i += NW * kWave) soff[i] = qoff[i];
 
     // files: wave-strided over the grid (persistent: ~2 workgroups per CU, tables loaded once)
@@ -168,15 +166,22 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         const int32_t lf = nx.lf;
         const uint32_t ccf = nx.cc != 0 ? 1u : 0u;
         if (PF && file + fstride < n) prune_load<J>(nx, rows, file + fstride, w64, wfp, lenp, ccp, lane);
-        // group g = lane / (64 / G): sums over 4 (8) lanes, two groups per dword
+        // group g = lane / 4: 4-lane sums (DPP quad_perm)
         pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
         pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-        if (G == 8) pc += (uint32_t)__builtin_amdgcn_ds_swizzle((int)pc, 0x101F);   // lane ^ 4
-        uint32_t fg[kGW];
+        uint32_t gs[kPruneGroups];
 #pragma unroll
-        for (int k = 0; k < kGW; ++k)
-            fg[k] = rfl(__builtin_amdgcn_readlane(pc, 2 * k * (64 / G)) |
-                        (__builtin_amdgcn_readlane(pc, (2 * k + 1) * (64 / G)) << 16));
+        for (int g = 0; g < kPruneGroups; ++g) gs[g] = rfl(__builtin_amdgcn_readlane(pc, 4 * g));
+        uint32_t wv = 0, gmax = 0;
+#pragma unroll
+        for (int g = 0; g < kPruneGroups; ++g) {
+            wv += gs[g];
+            gmax = max(gmax, gs[g]);
+        }
+        uint32_t fb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            fb[k] = gs[4 * k] | (gs[4 * k + 1] << 8) | (gs[4 * k + 2] << 16) | (gs[4 * k + 3] << 24);
         // a file outside the plain range (len_F < 0, |W_F| >= 2^30: never from real text) keeps
         // every template: all are scored exactly (int32 den stays as dice_den computes it)
         const bool plain = lf >= 0 && wf < (1u << 30);
@@ -185,30 +190,23 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         // lane keeps its two largest keys
         uint32_t key[TJ];
         uint32_t m1 = 0, m2 = 0;
+        const bool big = gmax > 255;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-            if (diag & 1) { key[j] = (j == 0 && lane == 0) ? 0x7F800001u : 0u; m1 = max(m1, key[j]); continue; }
             const int32_t t = lane + j * kWave;
             const uint4 c = stc[t];
-            uint32_t mn[kGW];
-#pragma unroll
-            for (int q = 0; q < kGW; q += 4) {
-                const uint4 a4 = sqa4[(q / 4) * kTP + t];
-                mn[q] = pk_min(a4.x, fg[q]);
-                mn[q + 1] = pk_min(a4.y, fg[q + 1]);
-                mn[q + 2] = pk_min(a4.z, fg[q + 2]);
-                mn[q + 3] = pk_min(a4.w, fg[q + 3]);
-            }
-#pragma unroll
-            for (int h = kGW / 2; h >= 1; h /= 2)   // pairwise u16 sums (short dependency chains)
-#pragma unroll
-                for (int q = 0; q < h; ++q) mn[q] = pk_add(mn[q], mn[q + h]);
-            const uint32_t m = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, mn[0]), (u16x2){1, 1}, 0u, false);
+            const uint4 a = q8[t];
+            uint32_t d = __builtin_amdgcn_sad_u8(a.x, fb[0], 0u);
+            d = __builtin_amdgcn_sad_u8(a.y, fb[1], d);
+            d = __builtin_amdgcn_sad_u8(a.z, fb[2], d);
+            d = __builtin_amdgcn_sad_u8(a.w, fb[3], d);
+            const uint32_t m = big ? wv : ((c.z >> 16) + wv - d) >> 1;
             const int32_t adj = max((int32_t)__usad(c.x, (uint32_t)lf, c.y), 0);
-            const int32_t den = (int32_t)(c.z + wf + ((uint32_t)adj >> 2));
+            const int32_t den = (int32_t)((c.z & 0xFFFFu) + wf + ((uint32_t)adj >> 2));
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)c.w, ccf, 1);   // 0 or ~0
             const uint32_t tp1 = (uint32_t)t + 1u;
-            const uint32_t k = keep & (plain ? bound_key(m, den, tp1) : (0x7F800000u | tp1));
+            uint32_t k = keep & (plain ? bound_key(m, den, tp1) : (0x7F800000u | tp1));
+            if (diag & 1) k = (j == 0 && lane == 0) ? 0x7F800001u : 0u;
             key[j] = k;
             m2 = max(m2, min(m1, k));
             m1 = max(m1, k);
@@ -268,23 +266,21 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
 
 static int32_t prune_tj(int32_t T) { return T <= 640 ? 10 : (kPruneMaxT + kWave - 1) / kWave; }
 
-static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T, int32_t groups) {
+static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
     const size_t tp = (size_t)prune_tj(T) * kWave;
-    return (size_t)nw * w64 * 8 + tp * (groups / 2) * 4 + tp * 16 + ((size_t)T + 1) * 4;
+    return (size_t)nw * w64 * 8 + tp * 16 + tp * 16 + ((size_t)T + 1) * 4;
 }
 
 int prune_setup(dice_ctx* c, const dice_templates* t) {
     const char* e = getenv("DICE_POST_PRUNE");
     if (e && *e == '0') return DICE_OK;
-    const char* eg = getenv("DICE_PRUNE_GROUPS");
-    const int32_t G = eg && *eg && atoi(eg) == 8 ? 8 : kPruneGroups;
     const int32_t T = c->T, w64 = c->w64;
-    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T, G) > 160 * 1024)
+    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024)
         return DICE_OK;
     const size_t tp = (size_t)prune_tj(T) * kWave;
-    // group counts |Lf_t ∩ g| (< 2^16: post_feasible bounds |Lf|) as u16 pairs, the constants,
-    // records of the nonzero u64 words; padding templates have keep bits 0
-    std::vector<uint32_t> qa(tp * (G / 2), 0);
+    // group counts A_g = |Lf_t ∩ g| clamped to bytes, one [tp] uint4 table; the constants;
+    // records of the nonzero u64 words. Padding templates have keep bits 0.
+    std::vector<uint32_t> q8(tp * 4, 0);
     std::vector<uint4> tcv(tp, make_uint4(0, 0, 0, 0));
     std::vector<uint32_t> qoff((size_t)T + 1, 0);
     std::vector<uint4> qrec;
@@ -293,24 +289,29 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
         uint32_t gc[kPruneGroups] = {0};
         for (int32_t p = 0; p < w64; ++p) {
             if (!r[p]) continue;
-            gc[(p % kWave) / (kWave / G)] += (uint32_t)__builtin_popcountll(r[p]);
+            gc[(p % kWave) / (kWave / kPruneGroups)] += (uint32_t)__builtin_popcountll(r[p]);
             qrec.push_back(make_uint4((uint32_t)p, (uint32_t)r[p], (uint32_t)(r[p] >> 32), 0));
         }
-        for (int k = 0; k < G / 2; ++k)   // [G / 8][tp] uint4 planes
-            qa[((size_t)(k / 4) * tp + (size_t)i) * 4 + (k % 4)] = gc[2 * k] | (gc[2 * k + 1] << 16);
+        uint32_t sum8 = 0;
+        for (int g = 0; g < kPruneGroups; ++g) {
+            const uint32_t a8 = std::min<uint32_t>(gc[g], 255u);
+            sum8 += a8;
+            q8[(size_t)i * 4 + g / 4] |= a8 << (8 * (g % 4));
+        }
         qoff[(size_t)i + 1] = (uint32_t)qrec.size();
         const int32_t slack = t->length_slack[i];
         tcv[(size_t)i] = make_uint4((uint32_t)t->length[i], (uint32_t)(-std::max(slack, 0)),
-                                    t->lf_size[i] - t->fields_set_size[i],
+                                    (t->lf_size[i] - t->fields_set_size[i]) | (sum8 << 16),
                                     (t->is_cc[i] ? 1u : 3u) | ((uint32_t)(slack & 0xFFFF) << 16));
     }
     if (qrec.empty()) qrec.push_back(make_uint4(0, 0, 0, 0));
     int rc;
-    if ((rc = dalloc_bytes(&c->d_qa, qa.size() * 4)) || (rc = dalloc_bytes(&c->d_qoff, qoff.size() * 4)) ||
+    if ((rc = dalloc_bytes(&c->d_q8, q8.size() * 4)) ||
+        (rc = dalloc_bytes(&c->d_qoff, qoff.size() * 4)) ||
         (rc = dalloc_bytes(&c->d_qrec, qrec.size() * sizeof(uint4))) ||
         (rc = dalloc_bytes(&c->d_qtc, tcv.size() * sizeof(uint4))))
         return rc;
-    if (hipMemcpy(c->d_qa, qa.data(), qa.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(c->d_q8, q8.data(), q8.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_qoff, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_qrec, qrec.data(), qrec.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_qtc, tcv.data(), tcv.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess)
@@ -318,7 +319,6 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     c->prune_records = (int64_t)qoff[(size_t)T];
     const char* sc = getenv("DICE_PRUNE_SCHED");
     c->prune_sched = sc && *sc ? atoi(sc) : 0;
-    c->prune_groups = G;
     const char* dg = getenv("DICE_PRUNE_DIAG");
     c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
@@ -327,17 +327,17 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
-template <int J, int TJ, int G, int NW, bool PF, int OCC>
+template <int J, int TJ, int NW, bool PF, int OCC>
 static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    const size_t lds = prune_lds_bytes(NW, c->w64, c->T, G);
-    auto kern = dice_prune_match<J, TJ, G, NW, PF, OCC>;
+    const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
+    auto kern = dice_prune_match<J, TJ, NW, PF, OCC>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
     // persistent grid: as many workgroups as are resident at once (LDS- and wave-limited)
     const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / NW, (160 * 1024) / (int64_t)lds));
     const int64_t groups = std::min<int64_t>((b->n + NW - 1) / NW, per_cu * c->n_cu);
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows,
-                       b->n, c->w64, c->T, (const uint32_t*)c->d_qa, (const uint4*)c->d_qtc,
+                       b->n, c->w64, c->T, (const uint4*)c->d_q8, (const uint4*)c->d_qtc,
                        (const uint32_t*)c->d_qoff, (const uint4*)c->d_qrec, b->d_wf, b->d_len, b->d_cc, thr,
                        b->d_best, b->d_ov, b->d_score, c->post_fast, c->prune_diag);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
@@ -346,22 +346,20 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
 // Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, row loads at the file;
 // 1 = 16-wave workgroups, the next file's row prefetched in VGPRs; 2 = 8-wave workgroups,
 // the next row prefetched (6 waves/SIMD); 3 = 8-wave workgroups, row loads at the file.
-template <int J, int TJ, int G>
+template <int J, int TJ>
 static int launch_prune_s(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     switch (c->prune_sched) {
-        case 1: return launch_prune<J, TJ, G, 16, true, 8>(c, b, thr, s);
-        case 2: return launch_prune<J, TJ, G, 8, true, 6>(c, b, thr, s);
-        case 3: return launch_prune<J, TJ, G, 8, false, 8>(c, b, thr, s);
-        default: return launch_prune<J, TJ, G, 16, false, 8>(c, b, thr, s);
+        case 1: return launch_prune<J, TJ, 16, true, 8>(c, b, thr, s);
+        case 2: return launch_prune<J, TJ, 8, true, 6>(c, b, thr, s);
+        case 3: return launch_prune<J, TJ, 8, false, 8>(c, b, thr, s);
+        default: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
     }
 }
 
 template <int J>
 static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     constexpr int kTJ11 = (kPruneMaxT + kWave - 1) / kWave;
-    if (c->prune_groups == 8)
-        return c->T <= 640 ? launch_prune_s<J, 10, 8>(c, b, thr, s) : launch_prune_s<J, kTJ11, 8>(c, b, thr, s);
-    return c->T <= 640 ? launch_prune_s<J, 10, 16>(c, b, thr, s) : launch_prune_s<J, kTJ11, 16>(c, b, thr, s);
+    return c->T <= 640 ? launch_prune_s<J, 10>(c, b, thr, s) : launch_prune_s<J, kTJ11>(c, b, thr, s);
 }
 
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {

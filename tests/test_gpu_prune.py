@@ -7,8 +7,9 @@ hash mode (the Set#& restatement of content_helper.rb:128-133) and against the p
 (DICE_POST_PRUNE=0), on:
 
   * the config-3 corpus (600 synthetic templates, V = 23,494) and its synthetic files;
-  * files that resemble no template (random bitsets: loose bounds, many exact scores), empty
-    files, CC-flagged files, files outside the fast envelope (|W_F| >= 2^20, len_F >= 2^21);
+  * files that resemble no template (random bitsets: loose bounds, many exact scores), files
+    with word-group counts above a byte (the coarse-bound fallback), empty files, CC-flagged
+    files, files outside the fast envelope (|W_F| >= 2^20, len_F >= 2^21);
   * exact ties: duplicated templates, where the later key must win (dice.rb:39);
   * a tiny vocabulary (one u64 word per lane) and T = 700 (11 templates per lane);
   * every schedule variant (DICE_PRUNE_SCHED) and ragged batch sizes.
@@ -122,6 +123,18 @@ def test_files_resembling_nothing(config3, monkeypatch):
     c, _ = config3
     fb = _random_files(c, 1500, seed=3, density=0.05)
     _check(c, fb, monkeypatch)
+
+
+def test_dense_files(config3, monkeypatch):
+    """Files holding a large share of the vocabulary: some word group counts exceed a byte, so the
+    kernel falls back to the coarse bound |W_F ∩ V| (and scores many templates exactly)."""
+    c, _ = config3
+    fb = _random_files(c, 300, seed=4, density=0.6)
+    counts = np.unpackbits(fb.bits.view(np.uint8), axis=1, bitorder='little').reshape(fb.n, -1, 64).sum(2)
+    groups = np.stack([counts[:, [p for p in range(counts.shape[1]) if (p % 64) // 4 == g]].sum(1)
+                       for g in range(16)], 1)
+    assert np.any(groups.max(1) > 255) and np.any(groups.max(1) <= 255)
+    _check(c, fb, monkeypatch, thresholds=(98.0, 0.0))
 
 
 def test_slow_envelope_files(config3, monkeypatch):
