@@ -190,7 +190,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         // lane keeps its two largest keys
         uint32_t key[TJ];
         uint32_t m1 = 0, m2 = 0;
-        const bool big = gmax > 255;
+        // uniform switches as masks (bitwise selects: no branches inside the unrolled pass, so
+        // the LDS reads of later templates are issued early)
+        const uint32_t bigm = gmax > 255 ? ~0u : 0u;
+        const uint32_t plainm = plain ? ~0u : 0u;
+        const uint32_t d1m = (diag & 1) ? ~0u : 0u;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
             const int32_t t = lane + j * kWave;
@@ -200,13 +204,14 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
             d = __builtin_amdgcn_sad_u8(a.y, fb[1], d);
             d = __builtin_amdgcn_sad_u8(a.z, fb[2], d);
             d = __builtin_amdgcn_sad_u8(a.w, fb[3], d);
-            const uint32_t m = big ? wv : ((c.z >> 16) + wv - d) >> 1;
+            const uint32_t m = (wv & bigm) | ((((c.z >> 16) + wv - d) >> 1) & ~bigm);
             const int32_t adj = max((int32_t)__usad(c.x, (uint32_t)lf, c.y), 0);
             const int32_t den = (int32_t)((c.z & 0xFFFFu) + wf + ((uint32_t)adj >> 2));
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)c.w, ccf, 1);   // 0 or ~0
             const uint32_t tp1 = (uint32_t)t + 1u;
-            uint32_t k = keep & (plain ? bound_key(m, den, tp1) : (0x7F800000u | tp1));
-            if (diag & 1) k = (j == 0 && lane == 0) ? 0x7F800001u : 0u;
+            const uint32_t bk = (bound_key(m, den, tp1) & plainm) | ((0x7F800000u | tp1) & ~plainm);
+            uint32_t k = keep & bk & ~d1m;
+            if (j == 0) k |= (lane == 0 ? 0x7F800001u : 0u) & d1m;
             key[j] = k;
             m2 = max(m2, min(m1, k));
             m1 = max(m1, k);
