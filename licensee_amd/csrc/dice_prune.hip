@@ -78,21 +78,40 @@ __device__ __forceinline__ uint32_t bound_key(uint32_t m, int32_t den, uint32_t 
     return ((__float_as_uint(fb) + kKeyLow) & ~kKeyLow) | tp1;
 }
 
-// Exact overlap of template ts with the wave's file row (one lane per record {u64 word, mask},
-// two records per lane in flight), its denominator and the running best in the strict
-// (score, later key) order; llo becomes an f32 lower bound of the best score.
-__device__ __forceinline__ void score_template(int32_t ts, const uint32_t* soff, const uint4* __restrict__ qrec,
+// Records of template ts: its first 128 (two per lane) are requested by records_head so their
+// latency overlaps other work; score_template finishes the overlap -- one lane per record {u64
+// word, mask} against the wave's file row in LDS -- takes the denominator and updates the running
+// best in the strict (score, later key) order; llo becomes an f32 lower bound of the best score.
+struct RecHead {
+    uint4 a, b;
+    uint32_t r0, r1;
+};
+
+__device__ __forceinline__ RecHead records_head(int32_t ts, const uint32_t* soff, const uint4* __restrict__ qrec,
+                                                int lane) {
+    RecHead h;
+    h.r0 = rfl(soff[ts]);
+    h.r1 = rfl(soff[ts + 1]);
+    const uint32_t r = h.r0 + lane;
+    h.a = r < h.r1 ? qrec[r] : make_uint4(0, 0, 0, 0);
+    h.b = r + kWave < h.r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+    return h;
+}
+
+__device__ __forceinline__ uint32_t rec_bits(const uint64_t* myrow, const uint4 a) {
+    const uint64_t f = myrow[a.x];
+    return (uint32_t)__builtin_popcount((uint32_t)f & a.y) + (uint32_t)__builtin_popcount((uint32_t)(f >> 32) & a.z);
+}
+
+__device__ __forceinline__ void score_template(int32_t ts, const RecHead& h, const uint4* __restrict__ qrec,
                                                const uint64_t* myrow, const uint4* stc, uint32_t wf, int32_t lf,
                                                bool fast, int lane, int32_t& bi, uint32_t& bo, int32_t& bd,
                                                float& llo) {
-    const uint32_t r0 = rfl(soff[ts]), r1 = rfl(soff[ts + 1]);
-    uint32_t acc = 0;
-    for (uint32_t r = r0 + lane; r < r1; r += 2 * kWave) {
+    uint32_t acc = rec_bits(myrow, h.a) + rec_bits(myrow, h.b);   // zero records read word 0, mask 0
+    for (uint32_t r = h.r0 + 2 * kWave + lane; r < h.r1; r += 2 * kWave) {   // > 128 records
         const uint4 a = qrec[r];
-        const uint4 b = r + kWave < r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
-        const uint64_t fa = myrow[a.x], fb = myrow[b.x];
-        acc += (uint32_t)__builtin_popcount((uint32_t)fa & a.y) + (uint32_t)__builtin_popcount((uint32_t)(fa >> 32) & a.z);
-        acc += (uint32_t)__builtin_popcount((uint32_t)fb & b.y) + (uint32_t)__builtin_popcount((uint32_t)(fb >> 32) & b.z);
+        const uint4 b = r + kWave < h.r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+        acc += rec_bits(myrow, a) + rec_bits(myrow, b);
     }
     const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
     const uint4 c = stc[ts];
@@ -227,13 +246,14 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         // second is below the first template's score, so is every other and the file is done
         const uint32_t K1 = rfl(__builtin_amdgcn_readlane(wave_incl_max(m1), kWave - 1));
         if (K1 != 0) {
+            const int32_t t1 = (int32_t)(K1 & kKeyLow) - 1;
+            const RecHead h1 = records_head(t1, soff, qrec, lane);   // in flight while K2 is found
             const uint32_t K2 = rfl(__builtin_amdgcn_readlane(wave_incl_max(m1 == K1 ? m2 : m1), kWave - 1));
-            if (diag & 2) { bi = (int32_t)(K1 & kKeyLow) - 1; bo = K2; } else
-            score_template((int32_t)(K1 & kKeyLow) - 1, soff, qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
+            if (diag & 2) { bi = t1; bo = K2; } else
+            score_template(t1, h1, qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
             if (!(diag & 2) && K2 != 0 && !(__uint_as_float(K2 & ~kKeyLow) < llo)) {
                 // more templates may reach the top: drop the scored one, then score the largest
                 // remaining key and drop every key below the best score, until none is left
-                const int32_t t1 = (int32_t)(K1 & kKeyLow) - 1;
                 if (lane == (t1 & (kWave - 1))) {
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
@@ -254,7 +274,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
                         for (int j = 0; j < TJ; ++j)
                             if (j == (ts >> 6)) key[j] = 0;
                     }
-                    score_template(ts, soff, qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
+                    score_template(ts, records_head(ts, soff, qrec, lane), qrec, myrow, stc, wf, lf, fast, lane, bi,
+                                   bo, bd, llo);
                 }
             }
         }
@@ -348,16 +369,16 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
 }
 
-// Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, row loads at the file;
-// 1 = 16-wave workgroups, the next file's row prefetched in VGPRs; 2 = 8-wave workgroups,
+// Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, the next file's row
+// prefetched in VGPRs; 1 = 16-wave workgroups, row loads at the file; 2 = 8-wave workgroups,
 // the next row prefetched (6 waves/SIMD); 3 = 8-wave workgroups, row loads at the file.
 template <int J, int TJ>
 static int launch_prune_s(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     switch (c->prune_sched) {
-        case 1: return launch_prune<J, TJ, 16, true, 8>(c, b, thr, s);
+        case 1: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
         case 2: return launch_prune<J, TJ, 8, true, 6>(c, b, thr, s);
         case 3: return launch_prune<J, TJ, 8, false, 8>(c, b, thr, s);
-        default: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
+        default: return launch_prune<J, TJ, 16, true, 8>(c, b, thr, s);
     }
 }
 
