@@ -88,8 +88,10 @@ def build_workload(config: int):
     return TemplateCorpus(templates)
 
 
-def traffic_for(cfg, n_per, T):
-    pmc_path = os.path.join(ROOT, 'profiles', f'pmc_config{cfg}.json')
+def traffic_for(cfg, n_per, T, variant=''):
+    """Per-launch HBM bytes from the committed PMC pass of this workload (variant '_post': config 3
+    on the postings kernels), or None."""
+    pmc_path = os.path.join(ROOT, 'profiles', f'pmc_config{cfg}{variant}.json')
     if not os.path.exists(pmc_path):
         return None, None
     try:
@@ -234,7 +236,7 @@ def parity_sample(run, orc, sptr, threads, n_sample):
 def measure_extra(r, c, args, stream, sptr, cpu):
     steps = min(args.steps, 20)
     w, lm, ach = timed(r, steps, 2, stream, False)
-    tr, tr_src = traffic_for(c, r.n_per, r.T) if r.match_kernel == r.kind or c == 5 else (None, None)
+    tr, tr_src = traffic_for(c, r.n_per, r.T, '_post' if (c == 3 and r.match_kernel == 3) else '')
     rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'templates': r.T, 'vocab': r.V,
            'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': r.n_per * steps / w,
            'scores_per_s': r.n_per * steps / w * r.T, 'launch_ms': lm,
@@ -305,7 +307,7 @@ def main():
     wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, distributed)
     total_files = n_per * world
     value = total_files * args.steps / wall
-    traffic, traffic_src = traffic_for(cfg, n_per, run.T)
+    traffic, traffic_src = traffic_for(cfg, n_per, run.T, '_post' if (cfg == 3 and run.match_kernel == 3) else '')
     batch, files, corpus, synth = run.batch, run.files, run.corpus, run.synth
 
     # ---- results: gathers (outside the timed region) -------------------------
