@@ -98,7 +98,7 @@ def traffic_for(cfg, n_per, T, variant=''):
         with open(pmc_path) as fh:
             pmc = json.load(fh)
         if pmc.get('files_per_launch') == n_per and pmc.get('templates') == T:
-            return pmc.get('hbm_bytes_per_launch'), f"profiles/pmc_config{cfg}.json ({pmc.get('tag')})"
+            return pmc.get('hbm_bytes_per_launch'), f"profiles/pmc_config{cfg}{variant}.json ({pmc.get('tag')})"
     except Exception:
         pass
     return None, None
