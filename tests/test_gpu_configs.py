@@ -98,24 +98,32 @@ def test_config4_full_size_properties(vendored):
     batch.matrix(3)
     mov, msc, tki, tks = batch.download_matrix(3)
     _topk_properties(corpus, fb, best, ov, score, mov, msc, tki, tks)
-    _sample_vs_oracle(_oracle(corpus), fb, best, ov, score, 20_000, seed=4)
+    # every file against the independent hash-set Set#& restatement
+    eb, eo, es = _oracle(corpus).match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0,
+                                       nthreads=16, mode=0)
+    assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
     batch.close()
     sc.close()
 
 
-@pytest.mark.parametrize('kernel', ['post', 'lds'])
+@pytest.mark.parametrize('kernel', ['post', 'post-allpairs', 'lds'])
 def test_config3_shard(kernel, monkeypatch):
+    """The 1.25M-file config-3 shard on each large-corpus match path: 'post' runs the bound-pruned
+    kernel (dice_prune.hip), checked on every file against the oracle's bitset mode (a full scan,
+    independent of the pruning) plus a hash-mode sample; 'post-allpairs' the postings kernels."""
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
     from licensee_amd.synth_templates import synthetic_templates
     for k in ('DICE_FORCE_DENSE', 'DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_LDS_G',
               'DICE_POST_DENSE'):
         monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv('DICE_LARGE_KERNEL', kernel)
+    monkeypatch.setenv('DICE_LARGE_KERNEL', 'lds' if kernel == 'lds' else 'post')
+    monkeypatch.setenv('DICE_POST_PRUNE', '0' if kernel == 'post-allpairs' else '1')
     corpus = TemplateCorpus(synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=20250202))
     fb = SyntheticCorpus(corpus).generate(0, 1_250_000, seed=20250202, nthreads=16)
     sc = _scorer(corpus)
-    assert sc.info()[2] == {'lds': 2, 'post': 3}[kernel]
+    assert sc.info()[2] == {'lds': 2, 'post': 3, 'post-allpairs': 3}[kernel]
+    assert sc.match_kernel() == {'lds': 2, 'post': 4, 'post-allpairs': 3}[kernel]
     batch = sc.batch(fb.n)
     batch.upload(fb)
     batch.match(98.0)
@@ -125,6 +133,10 @@ def test_config3_shard(kernel, monkeypatch):
     assert np.array_equal(best, b2) and np.array_equal(ov, o2) and np.array_equal(score, s2)
     assert ((best >= 0) == (score >= 98.0)).all() and best.max() < 600
     _sample_vs_oracle(_oracle(corpus), fb, best, ov, score, 20_000, seed=5)
+    if kernel == 'post':
+        eb, eo, es = _oracle(corpus).match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0,
+                                           nthreads=16, mode=1)
+        assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
     batch.close()
     # matrix/top-k on a 50k slice agrees with the match kernel's argmax
     s = _sub(fb, np.arange(50_000))

@@ -166,16 +166,11 @@ def test_full_size_match_vs_oracle_sample(big):
     assert np.array_equal(best, best2) and np.array_equal(ov, ov2) and np.array_equal(score, score2)
     orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
                        corpus.length, corpus.is_cc, corpus.n_vocab)
-    idx = np.random.default_rng(1).choice(fb.n, 100_000, replace=False)
-    idx.sort()
-    eb, eo, es = orc.match(fb.bits[idx], fb.wordset_size[idx], fb.length[idx], fb.cc_false_positive[idx], 98.0,
-                           nthreads=16, mode=1)
-    assert np.array_equal(best[idx], eb) and np.array_equal(ov[idx], eo) and np.array_equal(score[idx], es)
-    # and the independent hash-set Set#& restatement (no AND+popcount) on another 20k files
-    idx = np.sort(np.random.default_rng(2).choice(fb.n, 20_000, replace=False))
-    eb, eo, es = orc.match(fb.bits[idx], fb.wordset_size[idx], fb.length[idx], fb.cc_false_positive[idx], 98.0,
-                           nthreads=16, mode=0)
-    assert np.array_equal(best[idx], eb) and np.array_equal(ov[idx], eo) and np.array_equal(score[idx], es)
+    # every file, in the bitset mode and in the independent hash-set Set#& restatement (no
+    # AND+popcount; content_helper.rb:128-133)
+    for mode in (1, 0):
+        eb, eo, es = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=16, mode=mode)
+        assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es), mode
     assert ((best >= 0) == (score >= 98.0)).all()
     assert best.min() >= -1 and best.max() < len(corpus.templates)
 
