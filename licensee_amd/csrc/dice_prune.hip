@@ -140,7 +140,7 @@ __device__ __forceinline__ void score_template(int32_t ts, const RecHead& h, con
 //   m = (sum_g A'_g + sum_g F_g - sum_g |A'_g - F_g|) / 2          (16 B of table per template)
 // A file with some F_g > 255 (thousands of vocabulary words) uses the looser m = |W_F ∩ V|
 // (more templates are scored exactly; results are the same).
-template <int J, int TJ, int NW, bool PF, int OCC>
+template <int J, int TJ, int NW, bool PF, int OCC, bool V2>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void dice_prune_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint4* __restrict__ q8g, const uint4* __restrict__ tc, const uint32_t* __restrict__ qoff,
     const uint4* __restrict__ qrec, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
@@ -186,21 +186,35 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         const uint32_t ccf = nx.cc != 0 ? 1u : 0u;
         if (PF && file + fstride < n) prune_load<J>(nx, rows, file + fstride, w64, wfp, lenp, ccp, lane);
         // group g = lane / 4: 4-lane sums (DPP quad_perm)
+        const uint32_t pc0 = pc;
         pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
         pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-        uint32_t gs[kPruneGroups];
-#pragma unroll
-        for (int g = 0; g < kPruneGroups; ++g) gs[g] = rfl(__builtin_amdgcn_readlane(pc, 4 * g));
         uint32_t wv = 0, gmax = 0;
+        uint32_t fb[4];   // the 16 group counts as bytes (meaningful while every count <= 255)
+        if (V2) {
+            // bytes packed in VGPRs by row shifts (lane 16k + 12 holds groups 4k..4k+3), then
+            // 4 readlanes; |W_F ∩ V| and the largest group count by DPP reductions
+            uint32_t x = pc << 24;
+            x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x114, 0xf, 0xf, false) << 16;   // row_shr:4
+            x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x118, 0xf, 0xf, false) << 8;    // row_shr:8
+            x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x11C, 0xf, 0xf, false);         // row_shr:12
 #pragma unroll
-        for (int g = 0; g < kPruneGroups; ++g) {
-            wv += gs[g];
-            gmax = max(gmax, gs[g]);
+            for (int k = 0; k < 4; ++k) fb[k] = rfl(__builtin_amdgcn_readlane(x, 16 * k + 12));
+            wv = rfl(__builtin_amdgcn_readlane(wave_incl_scan(pc0), kWave - 1));
+            gmax = rfl(__builtin_amdgcn_readlane(wave_incl_max(pc), kWave - 1));
+        } else {
+            uint32_t gs[kPruneGroups];
+#pragma unroll
+            for (int g = 0; g < kPruneGroups; ++g) gs[g] = rfl(__builtin_amdgcn_readlane(pc, 4 * g));
+#pragma unroll
+            for (int g = 0; g < kPruneGroups; ++g) {
+                wv += gs[g];
+                gmax = max(gmax, gs[g]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                fb[k] = gs[4 * k] | (gs[4 * k + 1] << 8) | (gs[4 * k + 2] << 16) | (gs[4 * k + 3] << 24);
         }
-        uint32_t fb[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            fb[k] = gs[4 * k] | (gs[4 * k + 1] << 8) | (gs[4 * k + 2] << 16) | (gs[4 * k + 3] << 24);
         // a file outside the plain range (len_F < 0, |W_F| >= 2^30: never from real text) keeps
         // every template: all are scored exactly (int32 den stays as dice_den computes it)
         const bool plain = lf >= 0 && wf < (1u << 30);
@@ -214,6 +228,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
         const uint32_t bigm = gmax > 255 ? ~0u : 0u;
         const uint32_t plainm = plain ? ~0u : 0u;
         const uint32_t d1m = (diag & 1) ? ~0u : 0u;
+        const float kplain = plain ? 200.0f * 1.0000153f : __builtin_inff();
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
             const int32_t t = lane + j * kWave;
@@ -228,7 +243,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
             const int32_t den = (int32_t)((c.z & 0xFFFFu) + wf + ((uint32_t)adj >> 2));
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)c.w, ccf, 1);   // 0 or ~0
             const uint32_t tp1 = (uint32_t)t + 1u;
-            const uint32_t bk = (bound_key(m, den, tp1) & plainm) | ((0x7F800000u | tp1) & ~plainm);
+            uint32_t bk;
+            if (V2) {   // a non-plain file: x inf = +inf (or NaN): never dropped
+                const float fbd = fabsf((float)m * __builtin_amdgcn_rcpf((float)den)) * kplain;
+                bk = ((__float_as_uint(fbd) + kKeyLow) & ~kKeyLow) | tp1;
+            } else {
+                bk = (bound_key(m, den, tp1) & plainm) | ((0x7F800000u | tp1) & ~plainm);
+            }
             uint32_t k = keep & bk & ~d1m;
             if (j == 0) k |= (lane == 0 ? 0x7F800001u : 0u) & d1m;
             key[j] = k;
@@ -353,10 +374,10 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
-template <int J, int TJ, int NW, bool PF, int OCC>
+template <int J, int TJ, int NW, bool PF, int OCC, bool V2 = false>
 static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
-    auto kern = dice_prune_match<J, TJ, NW, PF, OCC>;
+    auto kern = dice_prune_match<J, TJ, NW, PF, OCC, V2>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
     // persistent grid: as many workgroups as are resident at once (LDS- and wave-limited)
@@ -370,15 +391,18 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
 }
 
 // Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, the next file's row
-// prefetched in VGPRs; 1 = 16-wave workgroups, row loads at the file; 2 = 8-wave workgroups,
-// the next row prefetched (6 waves/SIMD); 3 = 8-wave workgroups, row loads at the file.
+// prefetched in VGPRs, group counts packed by DPP and the non-plain case folded into the f32
+// key (V2); 1 = 16-wave workgroups, row loads at the file; 2 = 8-wave workgroups, the next row
+// prefetched (6 waves/SIMD); 3 = 8-wave workgroups, row loads at the file; 4 = as 0 without V2
+// (16 readlanes + scalar packing, a select for the non-plain case).
 template <int J, int TJ>
 static int launch_prune_s(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     switch (c->prune_sched) {
         case 1: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
         case 2: return launch_prune<J, TJ, 8, true, 6>(c, b, thr, s);
         case 3: return launch_prune<J, TJ, 8, false, 8>(c, b, thr, s);
-        default: return launch_prune<J, TJ, 16, true, 8>(c, b, thr, s);
+        case 4: return launch_prune<J, TJ, 16, true, 8, false>(c, b, thr, s);
+        default: return launch_prune<J, TJ, 16, true, 8, true>(c, b, thr, s);
     }
 }
 
