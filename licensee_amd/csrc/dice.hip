@@ -416,9 +416,11 @@ void dice_batch_destroy(dice_batch* b) {
     if (!b) return;
     DeviceGuard g(b->ctx->device);
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
-                    b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs};
+                    b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
+                    b->d_defer, b->d_ndefer};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (b->shadow) dice_batch_destroy(b->shadow);
     delete b;
 }
 

@@ -67,7 +67,7 @@ struct dice_ctx {
     void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
     void* d_qtc = nullptr;     // [padded T] uint4 template constants (dice_prune.hip)
     bool prune = false;
-    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0;
+    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8;
     int64_t prune_records = 0;
 };
 
@@ -117,4 +117,9 @@ struct dice_batch {
     int64_t* d_offs = nullptr;      // ... and its [capacity + 1] offsets
     size_t pdense_bytes = 0;
     size_t stage_bytes = 0;
+    // pruned match (dice_prune.hip): files deferred to the postings kernels, and the compact
+    // batch they are gathered into
+    int32_t* d_defer = nullptr;     // [capacity] file indices
+    uint32_t* d_ndefer = nullptr;   // count
+    dice_batch* shadow = nullptr;
 };

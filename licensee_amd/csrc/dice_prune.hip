@@ -42,6 +42,8 @@ constexpr int kPruneGroups = 16;         // word groups of the bound
 constexpr int kPruneMaxJ = 8;            // u64 words per lane: w64 <= 512 (V <= 32768)
 constexpr int kPruneMaxT = 704;          // = kPostMaxTpad (the key's low 10 bits hold the template)
 constexpr uint32_t kKeyLow = 1023u;
+constexpr int32_t kPruneMaxEvals = 8;     // default: exact scores per file before it is deferred to the postings kernels
+constexpr int64_t kDeferChunk = 65536;    // deferred files per postings pass
 
 
 
@@ -145,7 +147,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t T, const uint4* __restrict__ q8g, const uint4* __restrict__ tc, const uint32_t* __restrict__ qoff,
     const uint4* __restrict__ qrec, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
-    double* __restrict__ score_out, bool corpus_fast, int32_t diag) {
+    double* __restrict__ score_out, bool corpus_fast, int32_t diag, int32_t* __restrict__ defer,
+    uint32_t* __restrict__ ndefer, int32_t max_evals) {
     // diag (DICE_PRUNE_DIAG, diagnostics only -- results are wrong): 1 skips the bound pass (one
     // template scored), 2 skips exact scoring, 4 skips the row loads
     constexpr int kTP = TJ * kWave;   // padded template count
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
                     for (int j = 0; j < TJ; ++j)
                         if (j == (t1 >> 6)) key[j] = 0;
                 }
-                for (;;) {
+                for (int32_t evals = 1;; ++evals) {
                     uint32_t km = 0;
 #pragma unroll
                     for (int j = 0; j < TJ; ++j) {
@@ -289,6 +292,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
                     }
                     const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
                     if (K == 0) break;   // every template scored or dropped
+                    if (evals == max_evals) {   // max_evals 0: never
+                        // a file whose bounds stay loose (it resembles several templates or none:
+                        // stacked licenses, long notices) goes to the postings kernels instead
+                        if (lane == 0) defer[atomicAdd(ndefer, 1u)] = (int32_t)file;
+                        bi = -2;
+                        break;
+                    }
                     const int32_t ts = (int32_t)(K & kKeyLow) - 1;
                     if (lane == (ts & (kWave - 1))) {
 #pragma unroll
@@ -300,6 +310,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
                 }
             }
         }
+        if (bi == -2) continue;   // deferred: its results come from the postings kernels
         if (lane == 0) {
             const double s = bi >= 0 ? dice_score(bo, bd) : 0.0;
             best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
@@ -366,6 +377,8 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     c->prune_records = (int64_t)qoff[(size_t)T];
     const char* sc = getenv("DICE_PRUNE_SCHED");
     c->prune_sched = sc && *sc ? atoi(sc) : 0;
+    const char* me = getenv("DICE_PRUNE_MAX_EVALS");
+    c->prune_max_evals = me && *me ? std::max(0, atoi(me)) : kPruneMaxEvals;
     const char* dg = getenv("DICE_PRUNE_DIAG");
     c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
@@ -386,7 +399,8 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows,
                        b->n, c->w64, c->T, (const uint4*)c->d_q8, (const uint4*)c->d_qtc,
                        (const uint32_t*)c->d_qoff, (const uint4*)c->d_qrec, b->d_wf, b->d_len, b->d_cc, thr,
-                       b->d_best, b->d_ov, b->d_score, c->post_fast, c->prune_diag);
+                       b->d_best, b->d_ov, b->d_score, c->post_fast, c->prune_diag, b->d_defer, b->d_ndefer,
+                       c->prune_max_evals);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
 }
 
@@ -412,17 +426,76 @@ static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s)
     return c->T <= 640 ? launch_prune_s<J, 10>(c, b, thr, s) : launch_prune_s<J, kTJ11>(c, b, thr, s);
 }
 
+// Deferred files: gathered into the compact shadow batch, scored by the postings kernels, their
+// results scattered back.
+__global__ void dice_defer_gather(const int32_t* __restrict__ defer, int64_t c0, int64_t m, int32_t w64,
+                                  const uint64_t* __restrict__ rows, const uint32_t* __restrict__ wf,
+                                  const int32_t* __restrict__ len, const uint8_t* __restrict__ cc,
+                                  uint64_t* __restrict__ srows, uint32_t* __restrict__ swf, int32_t* __restrict__ slen,
+                                  uint8_t* __restrict__ scc) {
+    for (int64_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const int64_t f = defer[c0 + i];
+        for (int32_t w = threadIdx.x; w < w64; w += blockDim.x) srows[i * w64 + w] = rows[f * w64 + w];
+        if (threadIdx.x == 0) {
+            swf[i] = wf[f];
+            slen[i] = len[f];
+            scc[i] = cc[f];
+        }
+    }
+}
+
+__global__ void dice_defer_scatter(const int32_t* __restrict__ defer, int64_t c0, int64_t m,
+                                   const int32_t* __restrict__ sbest, const uint32_t* __restrict__ sov,
+                                   const double* __restrict__ sscore, int32_t* __restrict__ best,
+                                   uint32_t* __restrict__ ov, double* __restrict__ score) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t f = defer[c0 + i];
+        best[f] = sbest[i];
+        ov[f] = sov[i];
+        score[f] = sscore[i];
+    }
+}
+
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     if (b->n == 0) return DICE_OK;
-    switch ((c->w64 + kWave - 1) / kWave) {
-        case 1: return launch_prune_j<1>(c, b, thr, s);
-        case 2: return launch_prune_j<2>(c, b, thr, s);
-        case 3:
-        case 4: return launch_prune_j<4>(c, b, thr, s);
-        case 5:
-        case 6: return launch_prune_j<6>(c, b, thr, s);
-        default: return launch_prune_j<8>(c, b, thr, s);
+    int rc;
+    if (!b->d_defer) {
+        if ((rc = dalloc_bytes((void**)&b->d_defer, (size_t)b->capacity * 4)) ||
+            (rc = dalloc_bytes((void**)&b->d_ndefer, 4)))
+            return rc;
     }
+    if (hipMemsetAsync(b->d_ndefer, 0, 4, s) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
+    switch ((c->w64 + kWave - 1) / kWave) {
+        case 1: rc = launch_prune_j<1>(c, b, thr, s); break;
+        case 2: rc = launch_prune_j<2>(c, b, thr, s); break;
+        case 3:
+        case 4: rc = launch_prune_j<4>(c, b, thr, s); break;
+        case 5:
+        case 6: rc = launch_prune_j<6>(c, b, thr, s); break;
+        default: rc = launch_prune_j<8>(c, b, thr, s); break;
+    }
+    if (rc) return rc;
+    if (c->prune_max_evals == 0) return DICE_OK;   // no deferral
+    // the deferred count (a 4-byte read back; usually 0)
+    uint32_t m = 0;
+    if (hipMemcpyAsync(&m, b->d_ndefer, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return fail(DICE_E_DEVICE, "deferred-count read failed");
+    if (m == 0) return DICE_OK;
+    if (!b->shadow && (rc = dice_batch_create(c, std::min<int64_t>(kDeferChunk, b->capacity), &b->shadow))) return rc;
+    dice_batch* sh = b->shadow;
+    for (int64_t c0 = 0; c0 < (int64_t)m; c0 += sh->capacity) {
+        const int64_t k = std::min<int64_t>(sh->capacity, (int64_t)m - c0);
+        const unsigned gg = (unsigned)std::min<int64_t>(k, 4096);
+        hipLaunchKernelGGL(dice_defer_gather, dim3(gg), dim3(256), 0, s, b->d_defer, c0, k, c->w64,
+                           (const uint64_t*)b->d_rows, b->d_wf, b->d_len, b->d_cc, sh->d_rows, sh->d_wf, sh->d_len,
+                           sh->d_cc);
+        sh->n = k;
+        if ((rc = post_launch_match(c, sh, thr, s))) return rc;
+        hipLaunchKernelGGL(dice_defer_scatter, dim3((unsigned)std::min<int64_t>((k + 255) / 256, 4096)), dim3(256), 0, s,
+                           b->d_defer, c0, k, sh->d_best, sh->d_ov, sh->d_score, b->d_best, b->d_ov, b->d_score);
+        if (hipGetLastError() != hipSuccess) return fail(DICE_E_DEVICE, "deferred-file pass launch failed");
+    }
+    return DICE_OK;
 }
 
 }  // namespace dice

@@ -119,7 +119,12 @@ def _random_files(c, n, seed, density):
     return FileBatch(bits, wf, ln, cc)
 
 
-def test_files_resembling_nothing(config3, monkeypatch):
+@pytest.mark.parametrize('max_evals', ['8', '0', '1'])
+def test_files_resembling_nothing(config3, max_evals, monkeypatch):
+    """Loose bounds: with deferral (DICE_PRUNE_MAX_EVALS, default 8; 1 defers every file that
+    needs a second exact score) those files are gathered and scored by the postings kernels;
+    0 scores them all in the pruned kernel."""
+    monkeypatch.setenv('DICE_PRUNE_MAX_EVALS', max_evals)
     c, _ = config3
     fb = _random_files(c, 1500, seed=3, density=0.05)
     _check(c, fb, monkeypatch)
