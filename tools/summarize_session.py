@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PREFIXES = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune_')
+PREFIXES = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune_', 'dice_defer_')
 
 
 def base(name):
