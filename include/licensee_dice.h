@@ -127,8 +127,13 @@ int dice_similarity_matrix(dice_ctx *ctx, const dice_files *files,
  *                       the caller's buffers (parallel D2H);
  *   DICE_GATHER_DEVICE  every device copies its results into one buffer on ctxs[0]'s device
  *                       (peer copies over xGMI), then one D2H from there.
- * Several ctxs may share a device (tests on a one-GPU box). Results are bit-identical to the
- * single-ctx calls. Outputs as dice_match / dice_similarity_matrix. */
+ * The device gather enables peer access (hipDeviceEnablePeerAccess) from every shard's device
+ * to ctxs[0]'s first; where two devices have none the runtime stages the copy instead.
+ * Shard rows given in pageable memory are staged through two page-locked buffers per ctx
+ * (each shard thread copies its own slice), so the shards do not share the runtime's bounce
+ * buffers. Several ctxs may share a device (tests on a one-GPU box); the same ctx twice is
+ * DICE_E_ARG. Results are bit-identical to the single-ctx calls. Outputs as dice_match /
+ * dice_similarity_matrix. */
 #define DICE_GATHER_HOST 0
 #define DICE_GATHER_DEVICE 1
 int dice_match_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files, double threshold,
@@ -136,6 +141,11 @@ int dice_match_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *f
 int dice_similarity_matrix_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files,
                                    int32_t gather_mode, uint32_t *overlap, double *score, int32_t k,
                                    int32_t *topk_index, double *topk_score);
+/* The last sharded call on this thread: 1 = device gather, every shard on another device wrote
+ * into ctxs[0]'s device through peer access (shards on ctxs[0]'s own device count as local);
+ * 0 = device gather with at least one shard through the runtime's staged copy; -1 = host
+ * gather or no sharded call yet. */
+int32_t dice_last_gather_peer(void);
 
 /* ---- device-resident batches (inputs and results stay in HBM) ---------------------- */
 int dice_batch_create(dice_ctx *ctx, int64_t capacity, dice_batch **out);

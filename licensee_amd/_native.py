@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     'dice_batch_match', 'dice_batch_matrix', 'dice_batch_download_match',
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
     'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
-    'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids',
+    'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids', 'dice_last_gather_peer',
     'dice_ctx_match_kernel',
 )
 DICE_GATHER_HOST = 0
@@ -83,6 +83,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_match_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), ctypes.c_double, i32, vp, vp, vp]),
         'dice_similarity_matrix_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), i32, vp, vp, i32,
                                                           vp, vp]),
+        'dice_last_gather_peer': (i32, []),
         'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
         'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
     }
@@ -331,6 +332,12 @@ def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DIC
         _check(load_library().dice_match_sharded(arr, n_ctx, ctypes.byref(st), float(threshold), int(gather),
                                                  _ptr(best), _ptr(ov), _ptr(score)))
     return best, ov, score
+
+
+def last_gather_peer() -> int:
+    """``dice_last_gather_peer``: 1 when the last sharded call's device gather wrote every remote
+    shard through peer access, 0 when some went through a staged copy, -1 for a host gather."""
+    return int(load_library().dice_last_gather_peer())
 
 
 def matrix_sharded(scorers, files: FileBatch, k: int = 0, gather: int = DICE_GATHER_HOST):

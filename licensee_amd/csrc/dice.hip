@@ -311,6 +311,10 @@ static void ctx_free(dice_ctx* c) {
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
+    for (int i = 0; i < 2; ++i) {
+        if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
+        if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -489,6 +493,20 @@ int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
     return upload_tail(b, n, f->wordset_size, f->length, f->cc_false_positive, s);
 }
 
+}  // extern "C"
+
+// dice_batch_upload for rows the caller already copied into b->d_rows on stream `s` (the
+// sharded path's pinned staging): the scalars and the repack.
+int dice::upload_rows_resident(dice_batch* b, const dice_files* f, hipStream_t s) {
+    if (f->n_files < 0 || f->n_files > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
+    DeviceGuard g(b->ctx->device);
+    b->n = f->n_files;
+    if (b->n == 0) return DICE_OK;
+    return upload_tail(b, b->n, f->wordset_size, f->length, f->cc_false_positive, s);
+}
+
+extern "C" {
+
 int dice_batch_upload_ids(dice_batch* b, int64_t n, const int64_t* offsets, const void* ids, int32_t id_bytes,
                           const uint32_t* wordset_size, const int32_t* length, const uint8_t* cc, void* stream) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
@@ -584,11 +602,11 @@ int dice_batch_matrix(dice_batch* b, int32_t k, void* stream) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
     if (k < 0 || k > DICE_TOPK_MAX) return fail(DICE_E_ARG, "k out of range");
     dice_ctx* c = b->ctx;
+    b->k_used = k;   // also on an empty batch: a later download with this k must be accepted
     if (b->n == 0) return DICE_OK;
     DeviceGuard g(c->device);
     int rc = ensure_matrix(b, k);
     if (rc) return rc;
-    b->k_used = k;
     hipStream_t s = pick_stream(c, stream);
     const int64_t n_tiles = (b->n + kWave - 1) / kWave;
     const unsigned grid = (unsigned)((n_tiles + (kBlock / kWave) - 1) / (kBlock / kWave));

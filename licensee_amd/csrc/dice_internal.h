@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/licensee_dice.h"
@@ -19,6 +21,25 @@ std::string& last_error();
 inline int fail(int code, const std::string& msg) {
     last_error() = msg;
     return code;
+}
+
+// Diagnostic switches (DICE_*_DIAG) make results wrong by design (phase-skip and timing
+// builds). They are honoured only by a library built with -DDICE_DIAG; the
+// shipped library ignores them and says so once on stderr, so a stray variable in a production
+// environment cannot corrupt Dice#match output.
+inline const char* diag_env(const char* name) {
+    const char* v = getenv(name);
+    if (!v || !*v) return nullptr;
+#ifdef DICE_DIAG
+    return v;
+#else
+    static bool warned = false;
+    if (!warned) {
+        warned = true;
+        fprintf(stderr, "liblicensee_dice: %s=%s ignored (diagnostic switches need a -DDICE_DIAG build)\n", name, v);
+    }
+    return nullptr;
+#endif
 }
 
 inline int dalloc_bytes(void** p, size_t bytes) {
@@ -69,6 +90,12 @@ struct dice_ctx {
     bool prune = false;
     int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8;
     int64_t prune_records = 0;
+    // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
+    // two page-locked staging buffers for shard uploads from pageable caller memory
+    uint64_t peer_mask = 0;
+    void* h_stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    size_t h_stage_bytes = 0;
 };
 
 namespace dice {
@@ -80,6 +107,8 @@ int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s);
 int prune_setup(dice_ctx* c, const dice_templates* t);
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+// dice_batch_upload's tail (scalars, repack) for rows already copied to b->d_rows on `s`
+int upload_rows_resident(dice_batch* b, const dice_files* f, hipStream_t s);
 // the ctx's reusable batch for the host-buffer calls (grown on demand)
 int scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out);
 // result downloads to host memory or (kind hipMemcpyDefault) another device's memory;

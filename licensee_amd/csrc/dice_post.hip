@@ -567,7 +567,7 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
         hipMemcpy(c->d_ptc, tcv.data(), tcv.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "postings plan upload failed");
     c->post_dense = D;
-    const char* dg = getenv("DICE_POST_DIAG");
+    const char* dg = diag_env("DICE_POST_DIAG");
     c->post_diag = dg && *dg ? atoi(dg) : 0;
     c->post_tpad = tpad;
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,

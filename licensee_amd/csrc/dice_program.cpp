@@ -345,7 +345,7 @@ static std::string acc_quad(const std::vector<Entry>& dm, size_t b0, size_t end,
     const char* be = getenv("DICE_PROG_ACC_BLOCK");   // entries per asm block (4 measured best)
     const size_t kAccBlock = be && *be ? (size_t)std::max(1, std::min(16, atoi(be))) : 4;
     std::string out;
-    const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
+    const char* diag = diag_env("DICE_PROG_DIAG");   // diagnostics only: results are wrong
     if (diag && strcmp(diag, "noacc") == 0) return "acc[" + std::to_string(q) + " % NT] ^= f[0] ^ f[1] ^ f[2] ^ f[3];\n";
     for (size_t b = b0; b < end; b += kAccBlock) out += acc_block(dm, b, std::min(end, b + kAccBlock));
     return out;
@@ -571,7 +571,7 @@ std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool
         }
     }
     emit_macro(s, "FILE_PROLOGUE", prologue.str());
-    const char* diag = getenv("DICE_PROG_DIAG");   // diagnostics only: results are wrong
+    const char* diag = diag_env("DICE_PROG_DIAG");   // diagnostics only: results are wrong
     s << "#define WAVE_TIMING " << (diag && strcmp(diag, "timing") == 0 ? 1 : 0) << "\n";
     if (diag && strcmp(diag, "noepi") == 0) {
         std::ostringstream mb;

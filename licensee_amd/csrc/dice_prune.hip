@@ -379,7 +379,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     c->prune_sched = sc && *sc ? atoi(sc) : 0;
     const char* me = getenv("DICE_PRUNE_MAX_EVALS");
     c->prune_max_evals = me && *me ? std::max(0, atoi(me)) : kPruneMaxEvals;
-    const char* dg = getenv("DICE_PRUNE_DIAG");
+    const char* dg = diag_env("DICE_PRUNE_DIAG");
     c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
         c->n_cu = 256;

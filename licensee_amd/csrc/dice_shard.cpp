@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -30,6 +31,9 @@ int check_ctxs(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, int32_
         if (!ctxs[i]) return fail(DICE_E_ARG, "NULL ctx in ctxs");
         if (ctxs[i]->T != ctxs[0]->T || ctxs[i]->V != ctxs[0]->V)
             return fail(DICE_E_ARG, "ctxs hold different corpora (T or V differ)");
+        // each shard thread uses its ctx's scratch batch and stream: one ctx twice would race
+        for (int32_t j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return fail(DICE_E_ARG, "the same ctx appears twice in ctxs");
     }
     if (f->n_files < 0) return fail(DICE_E_ARG, "n_files < 0");
     return DICE_OK;
@@ -75,6 +79,81 @@ int run_shards(dice_ctx* const* ctxs, int32_t n_ctx, int64_t n, F&& fn) {
     return DICE_OK;
 }
 
+thread_local int32_t g_last_gather_peer = -1;
+
+// Page-locked memory? (the runtime DMAs it directly; pageable memory goes through its bounce
+// buffers, which the shard threads of one call would share)
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable: clear the sticky error
+        return false;
+    }
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+constexpr size_t kStageBytes = (size_t)32 << 20;   // per staging buffer (two per ctx)
+
+// Shard upload: the bitset rows from pageable caller memory go through the ctx's two pinned
+// staging buffers (memcpy of chunk i + 1 overlaps the DMA of chunk i); pinned or small inputs
+// are handed to dice_batch_upload as they are.
+int upload_shard(dice_ctx* c, dice_batch* b, const dice_files* part) {
+    const size_t row = (size_t)c->w64 * 8, bytes = (size_t)part->n_files * row;
+    if (bytes < 2 * kStageBytes || is_pinned(part->bits)) return dice_batch_upload(b, part, nullptr);
+    if (!c->h_stage[0]) {
+        for (int i = 0; i < 2; ++i) {
+            if (hipHostMalloc(&c->h_stage[i], kStageBytes, hipHostMallocDefault) != hipSuccess ||
+                hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming) != hipSuccess)
+                return fail(DICE_E_NOMEM, "pinned staging allocation failed");
+        }
+        c->h_stage_bytes = kStageBytes;
+    }
+    if (part->n_files > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
+    const int64_t per = (int64_t)(c->h_stage_bytes / row);
+    if (per < 1) return dice_batch_upload(b, part, nullptr);
+    const char* src = reinterpret_cast<const char*>(part->bits);
+    char* dst = reinterpret_cast<char*>(b->d_rows);
+    int k = 0;
+    for (int64_t f0 = 0; f0 < part->n_files; f0 += per, k ^= 1) {
+        const size_t nb = (size_t)std::min<int64_t>(per, part->n_files - f0) * row;
+        if (hipEventSynchronize(c->stage_ev[k]) != hipSuccess) return fail(DICE_E_DEVICE, "staging wait failed");
+        std::memcpy(c->h_stage[k], src + (size_t)f0 * row, nb);
+        if (hipMemcpyAsync(dst + (size_t)f0 * row, c->h_stage[k], nb, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipEventRecord(c->stage_ev[k], c->stream) != hipSuccess)
+            return fail(DICE_E_DEVICE, "staged H2D failed");
+    }
+    // the per-file scalars (9 B per file) and the tile repack, behind the rows on the stream
+    return dice::upload_rows_resident(b, part, c->stream);
+}
+
+// Peer access from device `from` to device `to` (tolerating an earlier enable); true when the
+// results of a shard on `from` can be written straight into `to`'s memory over xGMI.
+bool enable_peer(dice_ctx* from, int to) {
+    if (from->device == to) return true;
+    if (from->peer_mask >> to & 1) return true;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, from->device, to) != hipSuccess || !can) return false;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    bool ok = hipSetDevice(from->device) == hipSuccess;
+    if (ok) {
+        const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+        ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+        if (!ok) (void)hipGetLastError();
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (ok) from->peer_mask |= 1ull << to;
+    return ok;
+}
+
+// Before a device gather: peer access from every shard's device to ctxs[0]'s; records whether
+// all of them have it (dice_last_gather_peer).
+void prepare_device_gather(dice_ctx* const* ctxs, int32_t n_ctx) {
+    bool all = true;
+    for (int32_t i = 1; i < n_ctx; ++i) all = enable_peer(ctxs[i], ctxs[0]->device) && all;
+    g_last_gather_peer = all ? 1 : 0;
+}
+
 // Device gather buffer on ctxs[0]'s device: `bytes` bytes, freed by the caller.
 int gather_alloc(dice_ctx* c0, size_t bytes, void** p) {
     int prev = -1;
@@ -118,7 +197,11 @@ int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f
     if (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive) return fail(DICE_E_ARG, "NULL file arrays");
     const int32_t w64 = ctxs[0]->w64;
     char* dev = nullptr;
-    if (gather == DICE_GATHER_DEVICE && (rc = gather_alloc(ctxs[0], (size_t)n * 16, (void**)&dev))) return rc;
+    g_last_gather_peer = -1;
+    if (gather == DICE_GATHER_DEVICE) {
+        if ((rc = gather_alloc(ctxs[0], (size_t)n * 16, (void**)&dev))) return rc;
+        prepare_device_gather(ctxs, n_ctx);
+    }
     // device gather layout: best [n] i32 | overlap [n] u32 | score [n] f64
     int32_t* g_best = dev ? (int32_t*)dev : nullptr;
     uint32_t* g_ov = dev ? (uint32_t*)(dev + (size_t)n * 4) : nullptr;
@@ -129,7 +212,7 @@ int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f
         int r = dice::scratch_for(c, s.hi - s.lo, &b);
         if (r) return r;
         const dice_files part = slice(f, s.lo, s.hi, w64);
-        if ((r = dice_batch_upload(b, &part, nullptr)) || (r = dice_batch_match(b, thr, nullptr))) return r;
+        if ((r = upload_shard(c, b, &part)) || (r = dice_batch_match(b, thr, nullptr))) return r;
         if (dev)
             return dice::download_match_to(b, best ? g_best + s.lo : nullptr, ov ? g_ov + s.lo : nullptr,
                                            score ? g_score + s.lo : nullptr, c->stream, hipMemcpyDefault);
@@ -157,15 +240,18 @@ int dice_similarity_matrix_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const d
     // top-k index [n][k] i32 | top-k score [n][k] f64
     const size_t b_ov = (size_t)n * T * 4, b_sc = (size_t)n * T * 8, b_ki = (size_t)n * k * 4, b_ks = (size_t)n * k * 8;
     char* dev = nullptr;
-    if (gather == DICE_GATHER_DEVICE && (rc = gather_alloc(ctxs[0], b_ov + b_sc + b_ki + b_ks, (void**)&dev)))
-        return rc;
+    g_last_gather_peer = -1;
+    if (gather == DICE_GATHER_DEVICE) {
+        if ((rc = gather_alloc(ctxs[0], b_ov + b_sc + b_ki + b_ks, (void**)&dev))) return rc;
+        prepare_device_gather(ctxs, n_ctx);
+    }
     rc = run_shards(ctxs, n_ctx, n, [&](int32_t i, Shard& s) {
         dice_ctx* c = ctxs[i];
         dice_batch* b = nullptr;
         int r = dice::scratch_for(c, s.hi - s.lo, &b);
         if (r) return r;
         const dice_files part = slice(f, s.lo, s.hi, w64);
-        if ((r = dice_batch_upload(b, &part, nullptr)) || (r = dice_batch_matrix(b, k, nullptr))) return r;
+        if ((r = upload_shard(c, b, &part)) || (r = dice_batch_matrix(b, k, nullptr))) return r;
         const size_t lo = (size_t)s.lo;
         if (dev) {
             uint32_t* d_ov = (uint32_t*)dev;
@@ -185,5 +271,7 @@ int dice_similarity_matrix_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const d
     if (dev) (void)hipFree(dev);
     return rc;
 }
+
+int32_t dice_last_gather_peer(void) { return g_last_gather_peer; }
 
 }  // extern "C"

@@ -1,7 +1,9 @@
 """World-size-2 gloo test of the sharded path (licensee_amd/shard.py): disjoint shards by
-global file index, per-rank scoring (the C oracle stands in for the GPU scorer on CPU),
-results packed bit-exactly and all-gathered in shard order; the gathered result equals a
-single-process run over all files."""
+global file index, per-rank scoring, results packed bit-exactly and all-gathered in shard
+order; the gathered result equals a single-process oracle run over all files. Each rank scores
+through the HIP scorer where a GPU exists (the -m gpu case: both ranks on device 0 of the test
+box); the C oracle stands in for it only in the CPU case."""
+import pytest
 import os
 import socket
 
@@ -17,7 +19,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, n_per, out_path):
+def _worker(rank, world, port, n_per, out_path, use_gpu):
     import torch
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -31,9 +33,16 @@ def _worker(rank, world, port, n_per, out_path):
     corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
     first, count = shard_range(rank, world, n_per)
     fb = SyntheticCorpus(corpus).generate(first, count, seed=7, nthreads=2)
-    orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
-                       corpus.length, corpus.is_cc, corpus.n_vocab)
-    res = pack_results(*orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=2))
+    if use_gpu:
+        from licensee_amd._native import Scorer
+        sc = Scorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack, corpus.length,
+                    corpus.is_cc, corpus.n_vocab, device=0)
+        res = pack_results(*sc.match(fb, 98.0))
+        sc.close()
+    else:
+        orc = OracleScorer(corpus.lf_bits, corpus.lf_size, corpus.fields_set_size, corpus.length_slack,
+                           corpus.length, corpus.is_cc, corpus.n_vocab)
+        res = pack_results(*orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0, nthreads=2))
     out = all_gather_packed(torch.from_numpy(res))
     if rank == 0:
         np.save(out_path, out.numpy())
@@ -41,7 +50,8 @@ def _worker(rank, world, port, n_per, out_path):
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_gather(tmp_path):
+@pytest.mark.parametrize('use_gpu', [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_two_rank_shard_and_gather(tmp_path, use_gpu):
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.license import License
     from licensee_amd.shard import pack_results, unpack_results
@@ -49,7 +59,7 @@ def test_two_rank_shard_and_gather(tmp_path):
     from oracle.native import OracleScorer
     n_per, world = 3000, 2
     out_path = str(tmp_path / 'gathered.npy')
-    mp.start_processes(_worker, args=(world, _free_port(), n_per, out_path), nprocs=world, start_method='spawn')
+    mp.start_processes(_worker, args=(world, _free_port(), n_per, out_path, use_gpu), nprocs=world, start_method='spawn')
     gathered = np.load(out_path)
     corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
     fb = SyntheticCorpus(corpus).generate(0, world * n_per, seed=7, nthreads=2)

@@ -102,6 +102,50 @@ def test_sharded_rejects_mismatched_corpora(vendored):
     other.close()
 
 
+def test_sharded_rejects_duplicate_ctx(vendored):
+    """One ctx twice would make two shard threads share its scratch batch and stream."""
+    from licensee_amd._native import DiceError, match_sharded, matrix_sharded
+    corpus, fb, scs = vendored
+    with pytest.raises(DiceError, match='twice'):
+        match_sharded([scs[0], scs[0]], _sub(fb, 100), 98.0)
+    with pytest.raises(DiceError, match='twice'):
+        matrix_sharded([scs[1], scs[2], scs[1]], _sub(fb, 100), 3)
+
+
+def test_device_gather_reports_peer_path(vendored):
+    """Shards on ctxs[0]'s own device are local (1); a host gather reports -1."""
+    from licensee_amd._native import last_gather_peer, match_sharded
+    corpus, fb, scs = vendored
+    match_sharded(scs, _sub(fb, 1000), 98.0, 1)
+    assert last_gather_peer() == 1
+    match_sharded(scs, _sub(fb, 1000), 98.0, 0)
+    assert last_gather_peer() == -1
+
+
+def test_sharded_pinned_staging_large_pageable_input():
+    """Shards of more than 64 MB of pageable rows go through the ctx's two pinned staging
+    buffers in 32 MB chunks (several chunks per shard, odd remainder): results equal one
+    dice_match call on the same files, and page-locked inputs take the direct path."""
+    import torch
+    from licensee_amd._native import FileBatch, match_sharded
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.synth import SyntheticCorpus
+    corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    n = 400_037                                 # 448 B per file: 2 shards of ~90 MB
+    fb = SyntheticCorpus(corpus).generate(0, n, seed=17, nthreads=16)
+    scs = _scorers(corpus, 2)
+    ref = scs[0].match(fb, 98.0)
+    for gather in (0, 1):
+        for a, b in zip(match_sharded(scs, fb, 98.0, gather), ref):
+            assert np.array_equal(a, b)
+    pin = lambda a: torch.from_numpy(a).pin_memory().numpy()
+    pfb = FileBatch(pin(fb.bits), fb.wordset_size, fb.length, fb.cc_false_positive)
+    for a, b in zip(match_sharded(scs, pfb, 98.0, 0), ref):
+        assert np.array_equal(a, b)
+    for s in scs:
+        s.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
