@@ -162,8 +162,14 @@ int dice_batch_upload(dice_batch *batch, const dice_files *files, void *stream);
 int dice_batch_upload_ids(dice_batch *batch, int64_t n_files, const int64_t *offsets, const void *ids,
                           int32_t id_bytes, const uint32_t *wordset_size, const int32_t *length,
                           const uint8_t *cc_false_positive, void *stream);
-/* Kernel-only scoring of the resident batch (asynchronous on `stream`). */
+/* Kernel-only scoring of the resident batch, asynchronous on `stream`: no host synchronization
+ * and no device-to-host copy inside (capturable in a hipGraph). For T > 64 corpora this is the
+ * bound-pruned kernel followed by the postings kernels over the files it deferred; their count
+ * stays on the device. */
 int dice_batch_match(dice_batch *batch, double threshold, void *stream);
+/* Introspection after dice_batch_match (synchronizes `stream`): files the bound-pruned kernel
+ * deferred to the postings kernels in the last call (0 for other kernels). */
+int dice_batch_deferred(dice_batch *batch, int64_t *deferred, void *stream);
 /* Device-resident matrix results are template-major ([T][n] overlap/score, [k][n] top-k) so
  * every store is coalesced; dice_batch_download_matrix returns them row-major. */
 int dice_batch_matrix(dice_batch *batch, int32_t k, void *stream);

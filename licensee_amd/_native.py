@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = (
     'dice_batch_download_matrix', 'dice_batch_result_ptrs', 'dice_batch_bytes_per_file',
     'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
     'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids', 'dice_last_gather_peer',
+    'dice_batch_deferred',
     'dice_ctx_match_kernel',
 )
 DICE_GATHER_HOST = 0
@@ -84,6 +85,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_similarity_matrix_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), i32, vp, vp, i32,
                                                           vp, vp]),
         'dice_last_gather_peer': (i32, []),
+        'dice_batch_deferred': (ctypes.c_int, [vp, ctypes.POINTER(i64), vp]),
         'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
         'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
     }
@@ -297,6 +299,12 @@ class DeviceBatch:
                                                          _ptr(tki) if k else None, _ptr(tks) if k else None,
                                                          stream or None))
         return ov, score, tki, tks
+
+    def deferred(self, stream: int = 0) -> int:
+        """Files the bound-pruned kernel handed to the postings kernels in the last match."""
+        v = ctypes.c_int64(0)
+        _check(load_library().dice_batch_deferred(self._b, ctypes.byref(v), ctypes.c_void_p(stream) if stream else None))
+        return int(v.value)
 
     def result_ptrs(self):
         p = [ctypes.c_void_p() for _ in range(3)]

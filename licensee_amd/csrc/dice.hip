@@ -307,7 +307,7 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
     void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc,
-                    c->d_q8, c->d_qoff, c->d_qrec, c->d_qtc};
+                    c->d_q8, c->d_qoff, c->d_qrec, c->d_qtc, c->d_q3tc, c->d_q3cc};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -424,7 +424,6 @@ void dice_batch_destroy(dice_batch* b) {
                     b->d_defer, b->d_ndefer};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    if (b->shadow) dice_batch_destroy(b->shadow);
     delete b;
 }
 
@@ -442,7 +441,8 @@ int dice_batch_create(dice_ctx* ctx, int64_t capacity, dice_batch** out) {
     if ((rc = dalloc(&b->d_rows, (size_t)capacity * ctx->w64)) ||
         (rc = dalloc(&b->d_tiles, (size_t)b->n_tiles_cap * ctx->wq * kWave)) ||
         (rc = dalloc(&b->d_wf, npad)) || (rc = dalloc(&b->d_len, npad)) || (rc = dalloc(&b->d_cc, npad)) ||
-        (rc = dalloc(&b->d_best, npad)) || (rc = dalloc(&b->d_ov, npad)) || (rc = dalloc(&b->d_score, npad))) {
+        (rc = dalloc(&b->d_best, npad)) || (rc = dalloc(&b->d_ov, npad)) || (rc = dalloc(&b->d_score, npad)) ||
+        (ctx->prune && (rc = dice::prune_reserve(ctx, b)))) {
         dice_batch_destroy(b);
         return rc;
     }
@@ -704,6 +704,19 @@ int dice_batch_stream_probe(dice_batch* b, void* stream) {
     hipLaunchKernelGGL(dice_stream_probe, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
                        reinterpret_cast<uint4*>(b->d_rows));
     HIP_TRY(hipGetLastError());
+    return DICE_OK;
+}
+
+int dice_batch_deferred(dice_batch* b, int64_t* deferred, void* stream) {
+    if (!b || !deferred) return fail(DICE_E_ARG, "NULL batch/output");
+    *deferred = 0;
+    if (!b->d_ndefer || !b->ctx->prune) return DICE_OK;
+    DeviceGuard g(b->ctx->device);
+    uint32_t m = 0;
+    hipStream_t s = pick_stream(b->ctx, stream);
+    HIP_TRY(hipMemcpyAsync(&m, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *deferred = m;
     return DICE_OK;
 }
 

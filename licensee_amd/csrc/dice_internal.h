@@ -87,8 +87,11 @@ struct dice_ctx {
     void* d_qoff = nullptr;    // [T + 1] u32 record offsets
     void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
     void* d_qtc = nullptr;     // [padded T] uint4 template constants (dice_prune.hip)
-    bool prune = false;
-    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8;
+    void* d_q3tc = nullptr;    // [704] uint4 v3 constants {length, -max(slack, 0), 4 base - 3, sum of group bytes}
+    void* d_q3cc = nullptr;    // [704] u32 v3 CC masks (~0: a cc-* template)
+    bool prune = false, prune_zero_base = false;
+    uint32_t prune_wf_noclamp = 0;   // v3: |W_F| from which the bound's length term needs no clamp
+    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12;
     int64_t prune_records = 0;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
     // two page-locked staging buffers for shard uploads from pageable caller memory
@@ -105,8 +108,15 @@ bool post_feasible(const dice_templates* t);
 int post_setup(dice_ctx* c, const dice_templates* t);
 int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s);
+// the deferred files idx[0 .. *pn) of a pruned match (count on the device; no host read-back)
+int post_launch_match_indexed(dice_ctx* c, dice_batch* b, double thr, const int32_t* idx, const uint32_t* pn,
+                              hipStream_t s);
+// the batch's dense-partial buffer ([capacity][tp] u16)
+int post_reserve(dice_ctx* c, dice_batch* b);
 int prune_setup(dice_ctx* c, const dice_templates* t);
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+// the pruned match's device buffers for batch b (called by dice_batch_create)
+int prune_reserve(dice_ctx* c, dice_batch* b);
 // dice_batch_upload's tail (scalars, repack) for rows already copied to b->d_rows on `s`
 int upload_rows_resident(dice_batch* b, const dice_files* f, hipStream_t s);
 // the ctx's reusable batch for the host-buffer calls (grown on demand)
@@ -146,9 +156,7 @@ struct dice_batch {
     int64_t* d_offs = nullptr;      // ... and its [capacity + 1] offsets
     size_t pdense_bytes = 0;
     size_t stage_bytes = 0;
-    // pruned match (dice_prune.hip): files deferred to the postings kernels, and the compact
-    // batch they are gathered into
+    // pruned match (dice_prune.hip): files deferred to the postings kernels
     int32_t* d_defer = nullptr;     // [capacity] file indices
     uint32_t* d_ndefer = nullptr;   // count
-    dice_batch* shadow = nullptr;
 };

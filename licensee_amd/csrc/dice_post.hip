@@ -158,19 +158,24 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
 template <int DP, int TPMAX>
 __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(TPMAX <= 608 ? 8 : 4, TPMAX <= 608 ? 8 : 4))) void dice_post_dense(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
-    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ dense) {
+    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ dense, const int32_t* __restrict__ idx,
+    const uint32_t* __restrict__ pn) {
     __shared__ uint32_t stage32[kPostFiles * (TPMAX + 2) / 2];   // <= 78 KiB at TPMAX 608: 2 per CU
     uint16_t* st = reinterpret_cast<uint16_t*>(stage32);
     const int32_t cs = tp + 2;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
-    const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
+    // indexed (idx != NULL): the *pn files deferred by the pruned match, file i's row being
+    // rows[idx[i]] (persistent grid, count read on the device); partials stay indexed by i
+    const int64_t nn = idx ? (int64_t)*pn : n;
+    for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
     {
         const int64_t file = f0 + lane;
-        const bool valid = file < n;
+        const bool valid = file < nn;
+        const int64_t rf = valid && idx ? (int64_t)idx[file] : file;
         uint64_t fd[DP];
 #pragma unroll
-        for (int d = 0; d < DP; ++d) fd[d] = (valid && d < D) ? rows[file * w64 + d] : 0;
+        for (int d = 0; d < DP; ++d) fd[d] = (valid && d < D) ? rows[rf * w64 + d] : 0;
         const int32_t tw = (T + kPostWaves - 1) / kPostWaves;
         const int32_t tb = wave * tw, te = min(T, tb + tw);
         uint16_t* crow = st + lane * cs;
@@ -210,10 +215,12 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     __syncthreads();
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
         const int64_t file = f0 + fi;
-        if (file >= n) break;
+        if (file >= nn) break;
         const uint32_t* src = stage32 + (fi * cs) / 2;
         uint32_t* dst = reinterpret_cast<uint32_t*>(dense + file * tp);
         for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
+    }
+    __syncthreads();   // the stage is refilled by the next tile
     }
 }
 
@@ -357,11 +364,11 @@ struct FilePre {
     int32_t lf;
 };
 
-__device__ __forceinline__ void prefetch_file(int64_t file, const uint64_t* __restrict__ rows, int32_t w64,
+__device__ __forceinline__ void prefetch_file(int64_t pos, int64_t file, const uint64_t* __restrict__ rows, int32_t w64,
                                               int32_t pb0, const uint16_t* __restrict__ dense, int32_t tp,
                                               const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
                                               const uint8_t* __restrict__ ccp, int lane, FilePre& p) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + file * tp);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + pos * tp);
 #pragma unroll
     for (int j = 0; j < kPJ; ++j) {
         const int32_t i = lane + j * kWave;
@@ -392,7 +399,8 @@ __device__ __forceinline__ void post_narrow_body(
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
+    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
+    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
     // diag (DICE_POST_DIAG, diagnostics only -- results are wrong): 2 skips the postings walk,
     // 4 skips the narrow-word extraction, 8 skips scoring
     constexpr int kTJ = (TPMAX + kWave - 1) / kWave;           // templates per lane
@@ -403,18 +411,25 @@ __device__ __forceinline__ void post_narrow_body(
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
-    const int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
     uint32_t* crow32 = cnt32 + wave * TPMAX;
     for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
     for (int i = lane; i < TPMAX; i += kWave) crow32[i] = 0;
     __syncthreads();
 
     const int32_t pb0 = (diag & 4) ? w64 : D;
+    // indexed (idx != NULL, match mode): position i is the deferred file idx[i] of a pruned match
+    // (its dense partials at i, its row, scalars and results at idx[i]); persistent tiles
+    const int64_t nn = idx ? (int64_t)*pn : n;
+    for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
     FilePre pre;
-    if (f0 + wave < n) prefetch_file(f0 + wave, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
+    if (f0 + wave < nn) {
+        const int64_t p0 = f0 + wave;
+        prefetch_file(p0, idx ? (int64_t)idx[p0] : p0, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
+    }
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
-        const int64_t file = f0 + fi;
-        if (file >= n) break;   // wave-uniform
+        const int64_t pos = f0 + fi;
+        if (pos >= nn) break;   // wave-uniform
+        const int64_t file = idx ? (int64_t)rfl((uint32_t)idx[pos]) : pos;
         const uint64_t* row = rows + file * w64;
         // this file's dense partials start its counter row (a plain copy, u16 pairs widened: the
         // row is zero here and this wave's postings adds come after it)
@@ -431,12 +446,15 @@ __device__ __forceinline__ void post_narrow_body(
         for (int c = 0; c < kChunks; ++c) first[c] = POST_PREFETCH_WORDS ? pre.first[c] : 0;
         file_postings<kWCap>(row, w64, pb0, first, wq[wave], lq[wave], prow, plong, crow32, lane, diag);
         // the wave's next file: its independent loads fly while this one is scored
-        if (fi + kPostWaves < kPostFiles && file + kPostWaves < n)
-            prefetch_file(file + kPostWaves, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
+        if (fi + kPostWaves < kPostFiles && pos + kPostWaves < nn) {
+            const int64_t pn1 = pos + kPostWaves;
+            prefetch_file(pn1, idx ? (int64_t)idx[pn1] : pn1, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
+        }
 
         if (diag & 8) continue;
         score_file<kMatrix, KM, kTJ>(crow32, tcs, T, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
                                             k, mov, msc, tki, tks, lane);
+    }
     }
 }
 
@@ -449,9 +467,10 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
+    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
+    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
     post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, corpus_fast);
+                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn);
 }
 
 template <int KM, int TPMAX>
@@ -461,9 +480,10 @@ __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast) {
+    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
+    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
     post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, false);
+                               score_out, k, mov, msc, tki, tks, diag, false, idx, pn);
 }
 
 // ---- host side ---------------------------------------------------------------------------
@@ -581,21 +601,22 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     }
     c->post_tp = (T + 7) / 8 * 8;
     c->post_rows = nlong;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
+        c->n_cu = 256;
     c->kind = 3;
     return DICE_OK;
 }
 
 template <int DP>
-static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s) {
-    const int64_t groups = (b->n + kPostFiles - 1) / kPostFiles;
+static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t groups, const int32_t* idx,
+                         const uint32_t* pn) {
     auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
-                       (const uint64_t*)c->d_pdm, (uint16_t*)b->d_pdense);
+                       (const uint64_t*)c->d_pdm, (uint16_t*)b->d_pdense, idx, pn);
 }
 
-template <bool kMatrix, int KM>
-static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t s) {
+int post_reserve(dice_ctx* c, dice_batch* b) {
     const size_t need = (size_t)b->capacity * c->post_tp * 2;
     if (b->pdense_bytes < need) {
         if (b->d_pdense) (void)hipFree(b->d_pdense);
@@ -605,30 +626,49 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
         if (rc) return rc;
         b->pdense_bytes = need;
     }
+    return DICE_OK;
+}
+
+// idx/pn (match mode only): score the *pn files idx[0..*pn) of the batch (the pruned match's
+// deferred files) on persistent grids; nothing is read back on the host.
+template <bool kMatrix, int KM>
+static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t s, const int32_t* idx = nullptr,
+                  const uint32_t* pn = nullptr) {
+    int rc = post_reserve(c, b);
+    if (rc) return rc;
+    const int64_t tiles = (b->n + kPostFiles - 1) / kPostFiles;
+    // two workgroups per CU are resident in either kernel (LDS)
+    const int64_t groups = idx ? std::min<int64_t>(tiles, 2 * (int64_t)c->n_cu) : tiles;
     if (c->post_dense == 0 || (c->post_diag & 1)) {
-        if (hipMemsetAsync(b->d_pdense, 0, (size_t)b->n * c->post_tp * 2, s) != hipSuccess)
+        const int64_t rows = idx ? b->capacity : b->n;
+        if (hipMemsetAsync(b->d_pdense, 0, (size_t)rows * c->post_tp * 2, s) != hipSuccess)
             return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
     } else {
         switch ((c->post_dense + 3) / 4) {
-            case 1: launch_dense<4>(c, b, s); break;
-            case 2: launch_dense<8>(c, b, s); break;
-            case 3: launch_dense<12>(c, b, s); break;
-            default: launch_dense<16>(c, b, s); break;
+            case 1: launch_dense<4>(c, b, s, groups, idx, pn); break;
+            case 2: launch_dense<8>(c, b, s, groups, idx, pn); break;
+            case 3: launch_dense<12>(c, b, s, groups, idx, pn); break;
+            default: launch_dense<16>(c, b, s, groups, idx, pn); break;
         }
     }
-    const int64_t groups = (b->n + kPostFiles - 1) / kPostFiles;
     auto kern = c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608> : dice_post_narrow_match<608>)
                                   : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad> : dice_post_narrow_match<kPostMaxTpad>);
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
-                       b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_diag, c->post_fast);
+                       b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_diag, c->post_fast, idx,
+                       pn);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post kernels launch failed");
 }
 
 int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     return launch<false, 1>(c, b, thr, 0, s);
+}
+
+int post_launch_match_indexed(dice_ctx* c, dice_batch* b, double thr, const int32_t* idx, const uint32_t* pn,
+                              hipStream_t s) {
+    return launch<false, 1>(c, b, thr, 0, s, idx, pn);
 }
 
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s) {

@@ -43,7 +43,6 @@ constexpr int kPruneMaxJ = 8;            // u64 words per lane: w64 <= 512 (V <=
 constexpr int kPruneMaxT = 704;          // = kPostMaxTpad (the key's low 10 bits hold the template)
 constexpr uint32_t kKeyLow = 1023u;
 constexpr int32_t kPruneMaxEvals = 8;     // default: exact scores per file before it is deferred to the postings kernels
-constexpr int64_t kDeferChunk = 65536;    // deferred files per postings pass
 
 
 
@@ -55,7 +54,7 @@ struct PruneNext {
     int32_t lf;
 };
 
-template <int J>
+template <int J, bool TAIL2 = false>
 __device__ __forceinline__ void prune_load(PruneNext<J>& nx, const uint64_t* __restrict__ rows, int64_t file,
                                            int32_t w64, const uint32_t* __restrict__ wfp,
                                            const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp,
@@ -63,8 +62,9 @@ __device__ __forceinline__ void prune_load(PruneNext<J>& nx, const uint64_t* __r
     const uint64_t* row = rows + file * w64;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
+        // TAIL2: w64 > 64 (J - 2), so only the last two word slots can run past the row
         const int32_t p = lane + j * kWave;
-        nx.w[j] = p < w64 ? __builtin_nontemporal_load(row + p) : 0;
+        nx.w[j] = (TAIL2 && j < J - 2) || p < w64 ? __builtin_nontemporal_load(row + p) : 0;
     }
     nx.wf = wfp[file];
     nx.lf = lenp[file];
@@ -320,28 +320,346 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
     }
 }
 
+// ---- v3: the default schedule ----------------------------------------------------------------
+//
+// Same bound and exactness argument as above, cheaper per (file, template) pair (16 VALU
+// instead of ~28) and per file:
+//   * per-template LDS constants C = {length, -max(slack, 0), 4 base - 3, sum_g A'_g}, so
+//       m2 = sum_g A'_g + wv - sum_g |A'_g - F_g| = 2 m      (the v_sad_u8 chain starts at -wv:
+//                                                             one v_sub_u32 after it)
+//       D4 = 4 base - 3 + 4 wf + max(|len_t - len_F| - slack, 0) <= 4 den   (Ruby's floor /4)
+//     and score = 200 ov / den <= 200 m / den <= 400 m2 / D4: the key is the f32 m2 / D4 with
+//     its low 10 bits replaced by t + 1 (truncated, not rounded: the drop test's lower bound of
+//     the best score carries the 2^-11 margin instead, so that per-pair work stays minimal);
+//   * each lane keeps its two largest keys with v_med3_u32 + v_max_u32;
+//   * files whose denominators could be 0 or whose scalars leave the plain range (len_F < 0,
+//     |W_F| >= 2^28) go to the postings kernels, so the pass needs no special cases;
+//   * a file whose every bound is 0 is resolved without an exact score (each kept template
+//     scores 0.0 exactly; the later key wins the tie): files resembling nothing;
+//   * after two exact scores, a file with more than `route_cands` templates still able to reach
+//     the top goes to the postings kernels at once (stacked licenses, long notices) instead of
+//     after max_evals exact scores (one file in twenty has a top-bound template that is not the
+//     winner, so a count after the first score would defer many files the second score settles);
+//   * each wave owns a contiguous block of files: results collect in lane (file mod 64) and leave
+//     as one f64 division and three coalesced stores per 64 files.
+constexpr float kLloScale = 0.499755859375f;   // 0.5 (1 - 2^-11): keys are in units of score / 400
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// The exact denominator from the v3 constants (dice_den: content_helper.rb:128-133,337-347).
+__device__ __forceinline__ int32_t den3(const uint4 c, uint32_t wf, uint32_t lf) {
+    const int32_t x = max((int32_t)__usad(c.x, lf, c.y), 0);
+    return (int32_t)((c.z + 3u) >> 2) + (int32_t)wf + (x >> 2);
+}
+
+// One pass over the lane's TJ templates (t = lane + 64 j): keys and the lane's two largest.
+// BIG: some file group count exceeds a byte, m2 = 2 |W_F ∩ V| for every template. CC: the file
+// is potential_false_positive? -- cc-* templates are masked (ccm = ~0 for them).
+template <int TJ, bool BIG, bool CC, bool CLAMP>
+__device__ __forceinline__ void bound_pass3(const uint4* q8, const uint4* stc, const uint32_t* ccm, int32_t T,
+                                            const uint32_t (&fb)[4], uint32_t negwv, uint32_t m2big, uint32_t lf,
+                                            uint32_t wf4, int lane, uint32_t (&key)[TJ], uint32_t& m1,
+                                            uint32_t& m2) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        const int32_t t = lane + j * kWave;
+        const uint4 c = stc[t];
+        uint32_t mm;
+        if (!BIG) {
+            const uint4 a = q8[t];
+            uint32_t d = __builtin_amdgcn_sad_u8(a.x, fb[0], negwv);
+            d = __builtin_amdgcn_sad_u8(a.y, fb[1], d);
+            d = __builtin_amdgcn_sad_u8(a.z, fb[2], d);
+            d = __builtin_amdgcn_sad_u8(a.w, fb[3], d);
+            mm = c.w - d;
+        } else {
+            mm = m2big;
+        }
+        // x = |len_t - len_F| - slack; without the clamp at 0 (|W_F| >= wf_noclamp: every D4 stays
+        // >= 1) D4 is a smaller, still positive, lower bound of 4 den
+        const uint32_t x0 = __usad(c.x, lf, c.y);
+        const uint32_t x = CLAMP ? (uint32_t)max((int32_t)x0, 0) : x0;
+        const uint32_t d4 = c.z + wf4 + x;
+        const float q = (float)mm * __builtin_amdgcn_rcpf((float)d4);
+        // the slot j + 1 in the low bits (a literal: no register per slot); the lane is recovered
+        // from the lanes' maxima (key_lane)
+        uint32_t k = (__float_as_uint(q) & ~kKeyLow) | (uint32_t)(j + 1);
+        if (CC) k &= ~ccm[t];
+        if (j >= TJ - 2 && (j + 1) * kWave > T) k = t < T ? k : 0u;   // padding (TJ - 2 < T / 64 by prune3_tj)
+        key[j] = k;
+        m2 = umed3(m1, m2, k);
+        m1 = max(m1, k);
+    }
+}
+
+// The template of the wave's largest key K (v3 keys hold the lane's slot j + 1): the lowest lane
+// whose own maximum is K (keys of one lane are distinct; equal keys in several lanes are equal
+// bounds, any of them may go first).
+__device__ __forceinline__ int32_t key_template(uint32_t K, uint32_t lane_max, int32_t& kl) {
+    kl = (int32_t)__builtin_ctzll(__ballot(lane_max == K));
+    return kl + (int32_t)((K & kKeyLow) - 1) * kWave;
+}
+
+__device__ __forceinline__ void score_template3(int32_t ts, const RecHead& h, const uint4* __restrict__ qrec,
+                                                const uint64_t* myrow, const uint4* __restrict__ tcg, uint32_t wf,
+                                                uint32_t lf, bool fast, int lane, int32_t& bi, uint32_t& bo,
+                                                int32_t& bd, float& llo) {
+    // the template's constants by a scalar load (ts is uniform): the denominator and the order
+    // compare run on the scalar unit while the records' bits are counted
+    const uint4 c = tcg[ts];
+    uint32_t acc = rec_bits(myrow, h.a) + rec_bits(myrow, h.b);   // zero records read word 0, mask 0
+    for (uint32_t r = h.r0 + 2 * kWave + lane; r < h.r1; r += 2 * kWave) {   // > 128 records
+        const uint4 a = qrec[r];
+        const uint4 b = r + kWave < h.r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+        acc += rec_bits(myrow, a) + rec_bits(myrow, b);
+    }
+    const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
+    const int32_t den = den3(c, wf, lf);
+    const bool better = fast ? outranks_t<true>(ts, ov, den, bi, bo, bd) : outranks_t<false>(ts, ov, den, bi, bo, bd);
+    if (better) {
+        bi = ts;
+        bo = ov;
+        bd = den;
+        // f32 lower bound of best / 400 with a 2^-11 margin (covers the keys' truncation and
+        // every f32 rounding on both sides); den >= 1 on this path
+        llo = (float)bo * __builtin_amdgcn_rcpf((float)bd) * kLloScale;
+    }
+}
+
+template <int J, int TJ, int NW>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_prune3(
+    const uint64_t* __restrict__ rows, int64_t n, int64_t per_wave, int32_t w64, int32_t T,
+    const uint4* __restrict__ q8g, const uint4* __restrict__ tcg, const uint32_t* __restrict__ ccg,
+    const uint32_t* __restrict__ qoff, const uint4* __restrict__ qrec, const uint32_t* __restrict__ wfp,
+    const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out,
+    uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast, bool zero_base,
+    uint32_t wf_noclamp, int32_t* __restrict__ defer, uint32_t* __restrict__ ndefer, int32_t max_evals,
+    int32_t route_cands) {
+    constexpr int kTP = TJ * kWave;
+    // LDS: [waves][J * 64] file rows | [kTP] uint4 group bytes | [kTP] uint4 constants | [kTP] cc
+    // masks | [T + 1] record offsets
+    extern __shared__ uint64_t lds[];
+    uint4* q8 = reinterpret_cast<uint4*>(lds + (size_t)NW * J * kWave);
+    uint4* stc = q8 + kTP;
+    uint32_t* ccm = reinterpret_cast<uint32_t*>(stc + kTP);
+    uint32_t* soff = ccm + kTP;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    uint64_t* myrow = lds + (size_t)wave * J * kWave;
+    for (int i = threadIdx.x; i < kTP; i += NW * kWave) {
+        q8[i] = q8g[i];
+        stc[i] = tcg[i];
+        ccm[i] = ccg[i];
+    }
+    for (int i = threadIdx.x; i <= T; i += NW * kWave) soff[i] = qoff[i];
+
+    // the wave's contiguous block of files
+    const int64_t wbeg = ((int64_t)blockIdx.x * NW + wave) * per_wave;
+    const int64_t wend = min(n, wbeg + per_wave);
+    PruneNext<J> nx;
+    if (wbeg < wend) prune_load<J, true>(nx, rows, wbeg, w64, wfp, lenp, ccp, lane);
+    __syncthreads();
+
+    int32_t ri = -2, rd = 1;   // lane l: result of file (block start + l); -2 = none, -3 = deferred
+    uint32_t ro = 0;
+    for (int64_t file = wbeg; file < wend; ++file) {   // wave-uniform
+        const int slot = (int)((file - wbeg) & (kWave - 1));
+        uint32_t pc = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {   // the row buffer holds J * 64 words: no bounds test
+            myrow[lane + j * kWave] = nx.w[j];
+            pc += (uint32_t)__builtin_popcountll(nx.w[j]);
+        }
+        const uint32_t wf = nx.wf;
+        const int32_t lfi = nx.lf;
+        const uint32_t lf = (uint32_t)lfi;
+        const bool ccf = nx.cc != 0;
+        // the row is in LDS and counted before the next row's loads reuse its registers (else the
+        // scheduler hoists those loads above the LDS writes: 24 row VGPRs live, spills at 64)
+        __builtin_amdgcn_sched_barrier(0);
+        if (file + 1 < wend) prune_load<J, true>(nx, rows, file + 1, w64, wfp, lenp, ccp, lane);
+
+        int32_t bi = -1, bd = 1;
+        uint32_t bo = 0;
+        bool deferred = false;
+        // outside the plain range, or a possible zero denominator: the postings kernels
+        if (lfi < 0 || wf >= (1u << 28) || (zero_base && wf == 0)) {
+            deferred = true;
+        } else {
+            const uint32_t pc0 = pc;
+            pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+            pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+            const bool big = __ballot(pc > 255u) != 0;
+            uint32_t fb[4] = {0, 0, 0, 0};
+            uint32_t negwv = 0, m2big = 0;
+            if (!big) {
+                // group counts as bytes (lane 16k + 12 holds groups 4k..4k+3), |W_F ∩ V| by v_sad_u8
+                uint32_t x = pc << 24;
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x114, 0xf, 0xf, false) << 16;   // row_shr:4
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x118, 0xf, 0xf, false) << 8;    // row_shr:8
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x11C, 0xf, 0xf, false);         // row_shr:12
+#pragma unroll
+                for (int k = 0; k < 4; ++k) fb[k] = rfl(__builtin_amdgcn_readlane(x, 16 * k + 12));
+                uint32_t wv = __builtin_amdgcn_sad_u8(fb[0], 0u, 0u);
+                wv = __builtin_amdgcn_sad_u8(fb[1], 0u, wv);
+                wv = __builtin_amdgcn_sad_u8(fb[2], 0u, wv);
+                wv = __builtin_amdgcn_sad_u8(fb[3], 0u, wv);
+                negwv = 0u - wv;
+            } else {
+                m2big = 2u * rfl(__builtin_amdgcn_readlane(wave_incl_scan(pc0), kWave - 1));
+            }
+            const uint32_t wf4 = 4u * wf;
+            uint32_t key[TJ];
+            uint32_t m1 = 0, m2 = 0;
+            if (!big && !ccf && wf >= wf_noclamp)
+                bound_pass3<TJ, false, false, false>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
+            else if (!big && !ccf)
+                bound_pass3<TJ, false, false, true>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
+            else if (!big)
+                bound_pass3<TJ, false, true, true>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
+            else if (!ccf)
+                bound_pass3<TJ, true, false, true>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
+            else
+                bound_pass3<TJ, true, true, true>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
+            // the file's row is read by other lanes below: LDS ops of a wave run in order
+            __builtin_amdgcn_wave_barrier();
+
+            const bool fast = corpus_fast && wf < (1u << 20) && lf < (1u << 21);
+            const uint32_t K1 = rfl(__builtin_amdgcn_readlane(wave_incl_max(m1), kWave - 1));
+            if (K1 != 0) {   // 0: every template masked (CC filter)
+                if ((K1 & ~kKeyLow) == 0) {
+                    // every bound is 0: every kept template overlaps nothing and scores 0.0 (den >= 1);
+                    // the later key wins the tie: the largest kept index (the highest lane in the
+                    // highest slot whose key is nonzero)
+                    const int32_t j1 = (int32_t)(K1 & kKeyLow) - 1;
+                    const int32_t t1 = 63 - (int32_t)__builtin_clzll(__ballot(m1 == K1)) + j1 * kWave;
+                    bi = t1;
+                    bd = den3(tcg[t1], wf, lf);
+                } else {
+                    float llo = -1.0f;   // lower bound of best / 400 (f32); keys below it are dropped
+                    int32_t l1;
+                    const int32_t t1 = key_template(K1, m1, l1);
+                    const RecHead h1 = records_head(t1, soff, qrec, lane);   // in flight while K2 is found
+                    score_template3(t1, h1, qrec, myrow, tcg, wf, lf, fast, lane, bi, bo, bd, llo);
+                    // any other key still at or above the best score? (each lane's largest other
+                    // key: a ballot, no wave reduction)
+                    const uint32_t o1 = lane == l1 ? m2 : m1;
+                    if (__ballot(o1 != 0 && !(__uint_as_float(o1) < llo)) != 0) {
+                        // more templates may reach the top: score the largest remaining key and drop
+                        // every key below the best score, until none is left
+                        if (lane == l1) {
+#pragma unroll
+                            for (int j = 0; j < TJ; ++j)
+                                if (j == (t1 >> 6)) key[j] = 0;
+                        }
+                        for (int32_t evals = 1;; ++evals) {
+                            uint32_t km = 0, live = 0;
+#pragma unroll
+                            for (int j = 0; j < TJ; ++j) {
+                                if (__uint_as_float(key[j]) < llo) key[j] = 0;
+                                km = max(km, key[j]);
+                                if (evals == 2) live += (uint32_t)__builtin_popcountll(__ballot(key[j] != 0));
+                            }
+                            const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
+                            if (K == 0) break;   // every template scored or dropped
+                            // a file whose bounds stay loose (it resembles several templates or none:
+                            // stacked licenses, long notices) goes to the postings kernels: after two
+                            // exact scores when more than route_cands templates can still reach the top,
+                            // else after max_evals
+                            if (evals == max_evals || (evals == 2 && (int32_t)live > route_cands)) {
+                                deferred = true;
+                                break;
+                            }
+                            int32_t ls;
+                            const int32_t ts = key_template(K, km, ls);
+                            if (lane == ls) {
+#pragma unroll
+                                for (int j = 0; j < TJ; ++j)
+                                    if (j == (ts >> 6)) key[j] = 0;
+                            }
+                            score_template3(ts, records_head(ts, soff, qrec, lane), qrec, myrow, tcg, wf, lf, fast,
+                                            lane, bi, bo, bd, llo);
+                        }
+                    }
+                }
+            }
+        }
+        if (deferred) bi = -3;
+        if (lane == slot) {
+            ri = bi;
+            ro = bo;
+            rd = bd;
+        }
+        if (slot == kWave - 1 || file + 1 == wend) {
+            // the block's results: one division and three coalesced stores per 64 files; its
+            // deferred files take one atomic for the block (a per-file atomic on the one counter
+            // serialized: 2.8 ms for 250k deferred long files)
+            const int64_t f = file - slot + lane;
+            const bool mine = lane <= slot;
+            if (mine && ri >= -1) {
+                const double s = ri >= 0 ? dice_score(ro, rd) : 0.0;
+                best_out[f] = (ri >= 0 && s >= thr) ? ri : -1;
+                ov_out[f] = ro;
+                score_out[f] = s;
+            }
+            const uint64_t dm = __ballot(mine && ri == -3);
+            if (dm) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(ndefer, (uint32_t)__builtin_popcountll(dm));
+                base = __builtin_amdgcn_readlane(base, 0);
+                if (mine && ri == -3) defer[base + lane_rank(dm)] = (int32_t)f;
+            }
+            ri = -2;
+        }
+    }
+}
+
 // ---- host side ---------------------------------------------------------------------------
 
+// the old schedules' padded template count (10 or 11 per lane), and v3's (ceil(T / 64) rounded
+// to an instantiated width)
 static int32_t prune_tj(int32_t T) { return T <= 640 ? 10 : (kPruneMaxT + kWave - 1) / kWave; }
+static int32_t prune3_tj(int32_t T) {
+    for (int32_t tj : {2, 4, 6, 8, 10}) if (T <= tj * kWave) return tj;
+    return (kPruneMaxT + kWave - 1) / kWave;
+}
 
 static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
     const size_t tp = (size_t)prune_tj(T) * kWave;
     return (size_t)nw * w64 * 8 + tp * 16 + tp * 16 + ((size_t)T + 1) * 4;
 }
+static int32_t prune3_j(int32_t w64) {
+    const int32_t jw = (w64 + kWave - 1) / kWave;
+    return jw <= 2 ? jw : jw <= 4 ? 4 : jw <= 6 ? 6 : 8;
+}
+static size_t prune3_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
+    const size_t tp = (size_t)prune3_tj(T) * kWave;
+    return (size_t)nw * prune3_j(w64) * kWave * 8 + tp * (16 + 16 + 4) + ((size_t)T + 1) * 4;
+}
+
+constexpr int32_t kRouteCands = 32;   // v3: candidates left after two exact scores above which a file is deferred
 
 int prune_setup(dice_ctx* c, const dice_templates* t) {
     const char* e = getenv("DICE_POST_PRUNE");
     if (e && *e == '0') return DICE_OK;
     const int32_t T = c->T, w64 = c->w64;
-    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024)
+    if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024 ||
+        prune3_lds_bytes(kPruneWaves, w64, T) > 160 * 1024)
         return DICE_OK;
-    const size_t tp = (size_t)prune_tj(T) * kWave;
-    // group counts A_g = |Lf_t ∩ g| clamped to bytes, one [tp] uint4 table; the constants;
-    // records of the nonzero u64 words. Padding templates have keep bits 0.
+    // every table padded to the largest template count (704): each schedule reads its prefix.
+    // Group counts A_g = |Lf_t ∩ g| clamped to bytes; the old and the v3 constants; the v3 CC
+    // masks; the records of the nonzero u64 words. Padding templates have keep bits 0.
+    const size_t tp = (size_t)kPruneMaxT;
     std::vector<uint32_t> q8(tp * 4, 0);
-    std::vector<uint4> tcv(tp, make_uint4(0, 0, 0, 0));
+    std::vector<uint4> tcv(tp, make_uint4(0, 0, 0, 0)), tc3(tp, make_uint4(0, 0, 0, 0));
+    std::vector<uint32_t> cc3(tp, 0);
     std::vector<uint32_t> qoff((size_t)T + 1, 0);
     std::vector<uint4> qrec;
+    bool zero_base = false;
     for (int32_t i = 0; i < T; ++i) {
         const uint64_t* r = t->lf_bits + (size_t)i * w64;
         uint32_t gc[kPruneGroups] = {0};
@@ -358,27 +676,46 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
         }
         qoff[(size_t)i + 1] = (uint32_t)qrec.size();
         const int32_t slack = t->length_slack[i];
-        tcv[(size_t)i] = make_uint4((uint32_t)t->length[i], (uint32_t)(-std::max(slack, 0)),
-                                    (t->lf_size[i] - t->fields_set_size[i]) | (sum8 << 16),
+        const uint32_t base = t->lf_size[i] - t->fields_set_size[i];   // post_feasible: 0 <= base < 2^16
+        zero_base = zero_base || base == 0;
+        tcv[(size_t)i] = make_uint4((uint32_t)t->length[i], (uint32_t)(-std::max(slack, 0)), base | (sum8 << 16),
                                     (t->is_cc[i] ? 1u : 3u) | ((uint32_t)(slack & 0xFFFF) << 16));
+        tc3[(size_t)i] = make_uint4((uint32_t)t->length[i], (uint32_t)(-std::max(slack, 0)), 4u * base - 3u, sum8);
+        cc3[(size_t)i] = t->is_cc[i] ? ~0u : 0u;
     }
     if (qrec.empty()) qrec.push_back(make_uint4(0, 0, 0, 0));
     int rc;
     if ((rc = dalloc_bytes(&c->d_q8, q8.size() * 4)) ||
         (rc = dalloc_bytes(&c->d_qoff, qoff.size() * 4)) ||
         (rc = dalloc_bytes(&c->d_qrec, qrec.size() * sizeof(uint4))) ||
-        (rc = dalloc_bytes(&c->d_qtc, tcv.size() * sizeof(uint4))))
+        (rc = dalloc_bytes(&c->d_qtc, tcv.size() * sizeof(uint4))) ||
+        (rc = dalloc_bytes(&c->d_q3tc, tc3.size() * sizeof(uint4))) ||
+        (rc = dalloc_bytes(&c->d_q3cc, cc3.size() * 4)))
         return rc;
     if (hipMemcpy(c->d_q8, q8.data(), q8.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_qoff, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_qrec, qrec.data(), qrec.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_qtc, tcv.data(), tcv.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(c->d_qtc, tcv.data(), tcv.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_q3tc, tc3.data(), tc3.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_q3cc, cc3.data(), cc3.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "pruned-match plan upload failed");
     c->prune_records = (int64_t)qoff[(size_t)T];
+    c->prune_zero_base = zero_base;
+    // |W_F| from which D4 = 4 base - 3 + 4 wf + (|len_t - len_F| - slack) >= 1 for every template
+    // without the clamp: 4 wf >= slack + 4 - 4 base
+    int64_t wnc = 0;
+    for (int32_t i = 0; i < T; ++i) {
+        const int64_t base = (int64_t)t->lf_size[i] - (int64_t)t->fields_set_size[i];
+        const int64_t need = (int64_t)std::max(t->length_slack[i], 0) + 4 - 4 * base;
+        wnc = std::max<int64_t>(wnc, (need + 3) / 4);
+    }
+    c->prune_wf_noclamp = (uint32_t)std::min<int64_t>(wnc, 1u << 30);
     const char* sc = getenv("DICE_PRUNE_SCHED");
     c->prune_sched = sc && *sc ? atoi(sc) : 0;
     const char* me = getenv("DICE_PRUNE_MAX_EVALS");
     c->prune_max_evals = me && *me ? std::max(0, atoi(me)) : kPruneMaxEvals;
+    const char* rt = getenv("DICE_PRUNE_ROUTE");
+    c->prune_route = rt && *rt ? std::max(0, atoi(rt)) : kRouteCands;
     const char* dg = diag_env("DICE_PRUNE_DIAG");
     c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
@@ -387,6 +724,8 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
+// Old schedules (DICE_PRUNE_SCHED 1-5, A/B against v3; instantiated for the config-3 shape
+// only: 6 u64 words per lane, 10 or 11 templates per lane).
 template <int J, int TJ, int NW, bool PF, int OCC, bool V2 = false>
 static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
@@ -404,98 +743,92 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_match launch failed");
 }
 
-// Schedule variants (DICE_PRUNE_SCHED, A/B): 0 = 16-wave workgroups, the next file's row
-// prefetched in VGPRs, group counts packed by DPP and the non-plain case folded into the f32
-// key (V2); 1 = 16-wave workgroups, row loads at the file; 2 = 8-wave workgroups, the next row
-// prefetched (6 waves/SIMD); 3 = 8-wave workgroups, row loads at the file; 4 = as 0 without V2
-// (16 readlanes + scalar packing, a select for the non-plain case).
-template <int J, int TJ>
-static int launch_prune_s(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+// 1 = round 2's default (16-wave workgroups, next row prefetched, DPP-packed group counts, the
+// non-plain case folded into the f32 key); 2 = 16-wave, row loads at the file; 3 = 8-wave
+// workgroups, next row prefetched; 4 = 8-wave, row loads at the file; 5 = as 1 with readlane packing.
+template <int TJ>
+static int launch_prune_old(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     switch (c->prune_sched) {
-        case 1: return launch_prune<J, TJ, 16, false, 8>(c, b, thr, s);
-        case 2: return launch_prune<J, TJ, 8, true, 6>(c, b, thr, s);
-        case 3: return launch_prune<J, TJ, 8, false, 8>(c, b, thr, s);
-        case 4: return launch_prune<J, TJ, 16, true, 8, false>(c, b, thr, s);
-        default: return launch_prune<J, TJ, 16, true, 8, true>(c, b, thr, s);
+        case 2: return launch_prune<6, TJ, 16, false, 8>(c, b, thr, s);
+        case 3: return launch_prune<6, TJ, 8, true, 6>(c, b, thr, s);
+        case 4: return launch_prune<6, TJ, 8, false, 8>(c, b, thr, s);
+        case 5: return launch_prune<6, TJ, 16, true, 8, false>(c, b, thr, s);
+        default: return launch_prune<6, TJ, 16, true, 8, true>(c, b, thr, s);
     }
+}
+
+template <int J, int TJ>
+static int launch_prune3(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    constexpr int NW = kPruneWaves;
+    const size_t lds = prune3_lds_bytes(NW, c->w64, c->T);
+    auto kern = dice_prune3<J, TJ, NW>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
+    // persistent: as many workgroups as are resident at once, each wave a contiguous block of files
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / NW, (160 * 1024) / (int64_t)lds));
+    const int64_t max_waves = per_cu * c->n_cu * NW;
+    const int64_t per_wave = std::max<int64_t>(1, (b->n + max_waves - 1) / max_waves);
+    const int64_t groups = ((b->n + per_wave - 1) / per_wave + NW - 1) / NW;
+    const int32_t max_evals = c->prune_max_evals == 0 ? INT32_MAX : c->prune_max_evals;
+    const int32_t route = c->prune_max_evals == 0 ? INT32_MAX : c->prune_route;
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows, b->n,
+                       per_wave, c->w64, c->T, (const uint4*)c->d_q8, (const uint4*)c->d_q3tc,
+                       (const uint32_t*)c->d_q3cc, (const uint32_t*)c->d_qoff, (const uint4*)c->d_qrec, b->d_wf,
+                       b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, c->post_fast, c->prune_zero_base,
+                       c->prune_wf_noclamp, b->d_defer, b->d_ndefer, max_evals, route);
+    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune3 launch failed");
 }
 
 template <int J>
-static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    constexpr int kTJ11 = (kPruneMaxT + kWave - 1) / kWave;
-    return c->T <= 640 ? launch_prune_s<J, 10>(c, b, thr, s) : launch_prune_s<J, kTJ11>(c, b, thr, s);
-}
-
-// Deferred files: gathered into the compact shadow batch, scored by the postings kernels, their
-// results scattered back.
-__global__ void dice_defer_gather(const int32_t* __restrict__ defer, int64_t c0, int64_t m, int32_t w64,
-                                  const uint64_t* __restrict__ rows, const uint32_t* __restrict__ wf,
-                                  const int32_t* __restrict__ len, const uint8_t* __restrict__ cc,
-                                  uint64_t* __restrict__ srows, uint32_t* __restrict__ swf, int32_t* __restrict__ slen,
-                                  uint8_t* __restrict__ scc) {
-    for (int64_t i = blockIdx.x; i < m; i += gridDim.x) {
-        const int64_t f = defer[c0 + i];
-        for (int32_t w = threadIdx.x; w < w64; w += blockDim.x) srows[i * w64 + w] = rows[f * w64 + w];
-        if (threadIdx.x == 0) {
-            swf[i] = wf[f];
-            slen[i] = len[f];
-            scc[i] = cc[f];
-        }
+static int launch_prune3_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    switch (prune3_tj(c->T)) {
+        case 2: return launch_prune3<J, 2>(c, b, thr, s);
+        case 4: return launch_prune3<J, 4>(c, b, thr, s);
+        case 6: return launch_prune3<J, 6>(c, b, thr, s);
+        case 8: return launch_prune3<J, 8>(c, b, thr, s);
+        case 10: return launch_prune3<J, 10>(c, b, thr, s);
+        default: return launch_prune3<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
     }
 }
 
-__global__ void dice_defer_scatter(const int32_t* __restrict__ defer, int64_t c0, int64_t m,
-                                   const int32_t* __restrict__ sbest, const uint32_t* __restrict__ sov,
-                                   const double* __restrict__ sscore, int32_t* __restrict__ best,
-                                   uint32_t* __restrict__ ov, double* __restrict__ score) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t f = defer[c0 + i];
-        best[f] = sbest[i];
-        ov[f] = sov[i];
-        score[f] = sscore[i];
-    }
+// Device buffers of the pruned match, allocated with the batch (dice_batch_create): deferred
+// file list + count, and the postings pass's dense partials.
+int prune_reserve(dice_ctx* c, dice_batch* b) {
+    int rc;
+    if (!b->d_defer && ((rc = dalloc_bytes((void**)&b->d_defer, (size_t)b->capacity * 4)) ||
+                        (rc = dalloc_bytes((void**)&b->d_ndefer, 4))))
+        return rc;
+    return post_reserve(c, b);
 }
 
+// Dice#match over the batch, asynchronous on `s`: the pruned kernel, then the postings kernels
+// over the files it deferred (their count stays on the device: persistent grids read it and
+// exit at once when it is 0).
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     if (b->n == 0) return DICE_OK;
     int rc;
-    if (!b->d_defer) {
-        if ((rc = dalloc_bytes((void**)&b->d_defer, (size_t)b->capacity * 4)) ||
-            (rc = dalloc_bytes((void**)&b->d_ndefer, 4)))
-            return rc;
-    }
+    if ((rc = prune_reserve(c, b))) return rc;
     if (hipMemsetAsync(b->d_ndefer, 0, 4, s) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
-    switch ((c->w64 + kWave - 1) / kWave) {
-        case 1: rc = launch_prune_j<1>(c, b, thr, s); break;
-        case 2: rc = launch_prune_j<2>(c, b, thr, s); break;
-        case 3:
-        case 4: rc = launch_prune_j<4>(c, b, thr, s); break;
-        case 5:
-        case 6: rc = launch_prune_j<6>(c, b, thr, s); break;
-        default: rc = launch_prune_j<8>(c, b, thr, s); break;
+    const int32_t jw = (c->w64 + kWave - 1) / kWave;
+    const bool old = c->prune_sched >= 1 && c->prune_sched <= 5 && (jw == 5 || jw == 6) && c->T > 576;
+    if (old) {
+        rc = c->T <= 640 ? launch_prune_old<10>(c, b, thr, s)
+                         : launch_prune_old<(kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
+        if (rc) return rc;
+        if (c->prune_max_evals == 0) return DICE_OK;   // the old schedules score every file in-kernel then
+    } else {
+        switch (jw) {
+            case 1: rc = launch_prune3_j<1>(c, b, thr, s); break;
+            case 2: rc = launch_prune3_j<2>(c, b, thr, s); break;
+            case 3:
+            case 4: rc = launch_prune3_j<4>(c, b, thr, s); break;
+            case 5:
+            case 6: rc = launch_prune3_j<6>(c, b, thr, s); break;
+            default: rc = launch_prune3_j<8>(c, b, thr, s); break;
+        }
+        if (rc) return rc;
     }
-    if (rc) return rc;
-    if (c->prune_max_evals == 0) return DICE_OK;   // no deferral
-    // the deferred count (a 4-byte read back; usually 0)
-    uint32_t m = 0;
-    if (hipMemcpyAsync(&m, b->d_ndefer, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-        return fail(DICE_E_DEVICE, "deferred-count read failed");
-    if (m == 0) return DICE_OK;
-    if (!b->shadow && (rc = dice_batch_create(c, std::min<int64_t>(kDeferChunk, b->capacity), &b->shadow))) return rc;
-    dice_batch* sh = b->shadow;
-    for (int64_t c0 = 0; c0 < (int64_t)m; c0 += sh->capacity) {
-        const int64_t k = std::min<int64_t>(sh->capacity, (int64_t)m - c0);
-        const unsigned gg = (unsigned)std::min<int64_t>(k, 4096);
-        hipLaunchKernelGGL(dice_defer_gather, dim3(gg), dim3(256), 0, s, b->d_defer, c0, k, c->w64,
-                           (const uint64_t*)b->d_rows, b->d_wf, b->d_len, b->d_cc, sh->d_rows, sh->d_wf, sh->d_len,
-                           sh->d_cc);
-        sh->n = k;
-        if ((rc = post_launch_match(c, sh, thr, s))) return rc;
-        hipLaunchKernelGGL(dice_defer_scatter, dim3((unsigned)std::min<int64_t>((k + 255) / 256, 4096)), dim3(256), 0, s,
-                           b->d_defer, c0, k, sh->d_best, sh->d_ov, sh->d_score, b->d_best, b->d_ov, b->d_score);
-        if (hipGetLastError() != hipSuccess) return fail(DICE_E_DEVICE, "deferred-file pass launch failed");
-    }
-    return DICE_OK;
+    return post_launch_match_indexed(c, b, thr, b->d_defer, b->d_ndefer, s);
 }
 
 }  // namespace dice

@@ -85,7 +85,7 @@ def test_config3_files(config3, monkeypatch):
     assert 0.3 < np.mean(best >= 0) < 0.9   # the workload matches some files, not all
 
 
-@pytest.mark.parametrize('sched', [0, 1, 2, 3, 4])
+@pytest.mark.parametrize('sched', [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize('n', [1, 63, 64, 65, 129, 1000])
 def test_schedules_and_ragged_batches(config3, sched, n, monkeypatch):
     from licensee_amd._native import FileBatch
