@@ -40,13 +40,15 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'license files scored/sec (whole node) vs all templates; % HBM roofline'
 HBM_PEAK_GBS = 8000.0
-DEFAULT_FILES = {2: 1_000_000, 3: 1_250_000, 4: 1_000_000, 5: 1_000_000}
+DEFAULT_FILES = {2: 1_000_000, 3: 1_250_000, 4: 1_000_000, 5: 1_000_000, '5-T600': 1_250_000}
 KERNELS = ['dense', 'sparse-program', 'lds-records', 'postings', 'bound-pruned']
 WORKLOADS = {2: 'config2: synthetic perturbed LICENSE files x 47 choosealicense.com templates, Dice#match thr 98',
              3: 'config3: synthetic files x ~600 synthetic templates, Dice#match thr 98, one GPU shard '
                 'of the 10M-file node run',
              4: 'config4: long/mixed COPYING files (2-6 templates + notices) x 47 templates',
-             5: 'config5: full N x T similarity matrix + top-k x 47 templates'}
+             5: 'config5: full N x T similarity matrix + top-k x 47 templates',
+             '5-T600': 'config5 at T ~ 600: full N x T similarity matrix + top-k, config-3 files x 600 synthetic '
+                       'templates (licensee detect closest licenses on a large corpus)'}
 
 
 def log(*a):
@@ -111,9 +113,14 @@ class Run:
         from licensee_amd._native import Scorer
         from licensee_amd.shard import shard_range
         from licensee_amd.synth import SyntheticCorpus
+        self.tag = cfg
+        if cfg == '5-T600':          # matrix mode over the config-3 corpus and files
+            cfg, corpus_cfg = 5, 3
+        else:
+            corpus_cfg = cfg
         self.cfg, self.n_per, self.args = cfg, n_per, args
         t0 = time.time()
-        self.corpus = build_workload(cfg)
+        self.corpus = build_workload(corpus_cfg)
         self.synth = SyntheticCorpus(self.corpus, profile=1 if cfg == 4 else 0)
         first, count = shard_range(rank, world, n_per)
         self.files = self.synth.generate(first, count, seed=20250202, nthreads=nthreads)
@@ -126,7 +133,9 @@ class Run:
         self.match_kernel = self.scorer.match_kernel() if cfg != 5 else self.kind
         self.batch = self.scorer.batch(n_per)
         out_bytes = self.T * 12 + args.topk * 12 if cfg == 5 else 16
-        self.algo_bytes_per_file = self.batch.bytes_per_file() + 4 + 4 + 1 + out_bytes
+        # the file bitset as the kernels read it: tile layout (T <= 64) or row-major rows (T > 64)
+        in_bytes = self.batch.bytes_per_file() if self.kind != 3 else 8 * ((self.V + 63) // 64)
+        self.algo_bytes_per_file = in_bytes + 4 + 4 + 1 + out_bytes
 
     def step(self, sptr):
         if self.args.probe:
@@ -222,7 +231,17 @@ def parity_sample(run, orc, sptr, threads, n_sample):
         mism = int(np.sum(best[sl] != eb) + np.sum(ov[sl] != eo) + np.sum(score[sl] != es))
         return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)',
                 'oracle_files_per_s': sl.stop / cpu_s}
-    ovm, scm, tki, tks = run.batch.download_matrix(run.args.topk, sptr)
+    if run.n_per > n_sample:
+        # the matrix of the sample only (a T ~ 600 matrix of the whole batch is ~9 GB): the same
+        # files scored again in a batch of their own
+        from licensee_amd._native import FileBatch
+        sb = run.scorer.batch(sl.stop)
+        sb.upload(FileBatch(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl]), sptr)
+        sb.matrix(run.args.topk, sptr)
+        ovm, scm, tki, tks = sb.download_matrix(run.args.topk, sptr)
+        sb.close()
+    else:
+        ovm, scm, tki, tks = run.batch.download_matrix(run.args.topk, sptr)
     t0 = time.perf_counter()
     mov, msc = orc.matrix(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl], nthreads=threads)
     cpu_s = time.perf_counter() - t0
@@ -231,6 +250,56 @@ def parity_sample(run, orc, sptr, threads, n_sample):
     mism += int(np.sum(scm[rows, tki[sl, 0]] != tks[sl, 0]))
     return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (matrix, hash Set#&)',
             'oracle_files_per_s': sl.stop / cpu_s}
+
+
+def single_file_latency(run, n_calls=400):
+    """The drop-in's per-call latency (license_file.rb:92-98 -> dice.rb:34-41 scores one file at a
+    time; INTEGRATION.md's Ruby override calls dice_similarity_matrix with n = 1): p50/p99 wall
+    time of dice_similarity_matrix and dice_match with n = 1 through ctypes (structs and outputs
+    prepared beforehand, as an FFI binding would hold them), beside the C port's per-file time on
+    one thread over the same files (oracle/dice_ref.c hash Set#&, no per-call overhead)."""
+    import ctypes
+    from licensee_amd._native import FileBatch, load_library
+    from oracle.native import bits_to_csr
+    lib = load_library()
+    f, T = run.files, run.T
+    n = min(n_calls, f.n)
+    singles = [FileBatch(f.bits[i:i + 1], f.wordset_size[i:i + 1], f.length[i:i + 1], f.cc_false_positive[i:i + 1])
+               for i in range(n)]
+    structs = [fb._struct() for fb in singles]
+    ov = np.empty(T, np.uint32)
+    sc = np.empty(T, np.float64)
+    tki = np.empty(3, np.int32)
+    tks = np.empty(3, np.float64)
+    b1 = np.empty(1, np.int32)
+    o1 = np.empty(1, np.uint32)
+    s1 = np.empty(1, np.float64)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ctx = run.scorer._ctx
+    out = {}
+    for name, call in (('matrix_n1', lambda st: lib.dice_similarity_matrix(ctx, ctypes.byref(st), p(ov), p(sc), 3,
+                                                                            p(tki), p(tks))),
+                       ('match_n1', lambda st: lib.dice_match(ctx, ctypes.byref(st), 98.0, p(b1), p(o1), p(s1)))):
+        for st in structs[:20]:
+            call(st)                      # warm: scratch batch, code paths
+        ts = []
+        for st in structs:
+            t0 = time.perf_counter()
+            rc = call(st)
+            ts.append(time.perf_counter() - t0)
+            assert rc == 0
+        ts = np.array(ts) * 1e6
+        out[name] = {'p50_us': float(np.percentile(ts, 50)), 'p99_us': float(np.percentile(ts, 99)),
+                     'mean_us': float(ts.mean())}
+    orc = oracle_for(run.corpus)
+    m = min(4000, f.n)
+    csr = bits_to_csr(f.bits[:m], run.corpus.n_vocab)
+    t0 = time.perf_counter()
+    orc.match(f.bits[:m], f.wordset_size[:m], f.length[:m], f.cc_false_positive[:m], 98.0, nthreads=1, mode=0, csr=csr)
+    out['port_1thread_us_per_file'] = (time.perf_counter() - t0) / m * 1e6
+    out['note'] = ('wall time per call incl. ctypes; the GPU path is upload + kernel + download + sync of one file; '
+                   'port = oracle/dice_ref.c, one thread, per file of a 4000-file run')
+    return out
 
 
 def measure_extra(r, c, args, stream, sptr, cpu):
@@ -246,9 +315,10 @@ def measure_extra(r, c, args, stream, sptr, cpu):
         rec['note'] = ('bound-pruned Dice#match: every (file, template) pair is decided, but only pairs whose '
                        'overlap bound can reach the top score are scored exactly (DESIGN.md 4); scores_per_s '
                        'counts decided pairs. 3-allpairs scores every pair')
+        rec['deferred_files'] = r.batch.deferred(sptr)
     if not args.no_cpu_baseline:
         rec['parity'] = parity_sample(r, oracle_for(r.corpus), sptr, cpu['threads'],
-                                      {3: 20_000, 4: 30_000, 5: 50_000}[c])
+                                      {3: 20_000, 4: 30_000, 5: 50_000, '5-T600': 10_000}[c])
         # the parity leg is the reference-equivalent CPU path on the same files: its rate
         rec['cpu_baseline'] = {'value': rec['parity'].pop('oracle_files_per_s'), 'unit': 'files/s',
                                'cores': cpu['threads'], 'kind': 'port',
@@ -270,7 +340,7 @@ def main():
     ap.add_argument('--topk', type=int, default=3)
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU-work budget of the baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--extra-configs', default='3,4,5',
+    ap.add_argument('--extra-configs', default='3,4,5,5-T600',
                     help="configs also measured at N=1 (reported under extras.configs); '' for none")
     ap.add_argument('--probe', action='store_true', help='diagnostic: stream-read the tiles only (read ceiling)')
     args = ap.parse_args()
@@ -391,6 +461,10 @@ def main():
                                     f'native (csrc/normalize.cpp) {nthreads} threads on 16000 byte strings '
                                     f'(avg {sum(map(len, big)) / len(big) / 1024:.1f} KiB)')
 
+    if rank == 0 and cfg != 5 and not args.probe:
+        torch.cuda.synchronize()
+        extras['single_file_us'] = single_file_latency(run)
+
     cpu_baseline = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -435,7 +509,7 @@ def main():
         run.close()
         run = None
         extras['configs'] = {}
-        for c in [int(x) for x in args.extra_configs.split(',') if x.strip()]:
+        for c in [int(x) if x.strip().isdigit() else x.strip() for x in args.extra_configs.split(',') if x.strip()]:
             if c == cfg:
                 continue
             r = Run(c, DEFAULT_FILES[c], 0, 1, dev, nthreads, args)

@@ -53,8 +53,10 @@ _lib = None
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load liblicensee_dice.so (raises if it was not built -- no fallback)."""
+    """Load liblicensee_dice.so (raises if it was not built -- no fallback). LICENSEE_DICE_LIB
+    names another build of the same library (A/B of compile-time kernel variants)."""
     global _lib
+    path = os.environ.get('LICENSEE_DICE_LIB', path)
     if _lib is not None:
         return _lib
     if not os.path.exists(path):

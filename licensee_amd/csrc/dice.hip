@@ -307,7 +307,8 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
     void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc,
-                    c->d_q8, c->d_qoff, c->d_qrec, c->d_qtc, c->d_q3tc, c->d_q3cc};
+                    c->d_q8, c->d_qoff, c->d_qrec, c->d_qtc, c->d_q3tc, c->d_q3cc, c->d_p4q8, c->d_p4tc,
+                    c->d_p4cc, c->d_p4off, c->d_p4rec, c->d_p4slot, c->d_p4orig};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);

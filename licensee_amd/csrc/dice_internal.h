@@ -91,6 +91,10 @@ struct dice_ctx {
     void* d_q3cc = nullptr;    // [704] u32 v3 CC masks (~0: a cc-* template)
     bool prune = false, prune_zero_base = false;
     uint32_t prune_wf_noclamp = 0;   // v3: |W_F| from which the bound's length term needs no clamp
+    // v4 (dice_prune4): the v3 tables in position (length-sorted) order, slot bounds, position map
+    void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
+         *d_p4slot = nullptr, *d_p4orig = nullptr;
+    int32_t p4_zkeep[2] = {-1, -1}, p4_zpos[2] = {0, 0};
     int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12;
     int64_t prune_records = 0;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and

@@ -360,8 +360,6 @@ constexpr int kPJ = (kPostMaxTpad / 2 + kWave - 1) / kWave;   // u32 partial pai
 struct FilePre {
     uint32_t part[kPJ];
     uint64_t first[kChunks];
-    uint32_t wf, cc;
-    int32_t lf;
 };
 
 __device__ __forceinline__ void prefetch_file(int64_t pos, int64_t file, const uint64_t* __restrict__ rows, int32_t w64,
@@ -382,9 +380,6 @@ __device__ __forceinline__ void prefetch_file(int64_t pos, int64_t file, const u
             p.first[c] = q < w64 ? row[q] : 0;
         }
     }
-    p.wf = wfp[file];
-    p.lf = lenp[file];
-    p.cc = ccp[file];
 }
 
 // Phases 2 + 3, one file per wave (16 waves x 4 files per workgroup). Each wave owns one u32
@@ -421,15 +416,24 @@ __device__ __forceinline__ void post_narrow_body(
     // (its dense partials at i, its row, scalars and results at idx[i]); persistent tiles
     const int64_t nn = idx ? (int64_t)*pn : n;
     for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
+    // the tile's file indices and scalars, lane l = tile file l, by vector loads; each file reads
+    // them with v_readlane. (Scalar loads of the next file's |W_F| / len_F shared lgkmcnt with the
+    // postings walk's LDS adds and reads, whose waits then stalled on HBM latency.)
+    const int64_t tpos = min(f0 + lane, nn - 1);
+    const uint32_t tfile = idx ? (uint32_t)idx[tpos] : (uint32_t)tpos;
+    const uint32_t twf = wfp[tfile];
+    const uint32_t tlen = (uint32_t)lenp[tfile];
+    const uint32_t tcc = ccp[tfile];
     FilePre pre;
     if (f0 + wave < nn) {
         const int64_t p0 = f0 + wave;
-        prefetch_file(p0, idx ? (int64_t)idx[p0] : p0, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
+        prefetch_file(p0, (int64_t)__builtin_amdgcn_readlane(tfile, wave), rows, w64, pb0, dense, tp, wfp, lenp, ccp,
+                      lane, pre);
     }
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
         const int64_t pos = f0 + fi;
         if (pos >= nn) break;   // wave-uniform
-        const int64_t file = idx ? (int64_t)rfl((uint32_t)idx[pos]) : pos;
+        const int64_t file = (int64_t)rfl(__builtin_amdgcn_readlane(tfile, fi));
         const uint64_t* row = rows + file * w64;
         // this file's dense partials start its counter row (a plain copy, u16 pairs widened: the
         // row is zero here and this wave's postings adds come after it)
@@ -438,9 +442,9 @@ __device__ __forceinline__ void post_narrow_body(
             const int32_t i = lane + j * kWave;
             if (i < tp / 2) *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
         }
-        const uint32_t wf = pre.wf;
-        const int32_t lf = pre.lf;
-        const bool cc = pre.cc != 0;
+        const uint32_t wf = rfl(__builtin_amdgcn_readlane(twf, fi));
+        const int32_t lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
+        const bool cc = __builtin_amdgcn_readlane(tcc, fi) != 0;
         uint64_t first[kChunks];
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) first[c] = POST_PREFETCH_WORDS ? pre.first[c] : 0;
@@ -448,7 +452,8 @@ __device__ __forceinline__ void post_narrow_body(
         // the wave's next file: its independent loads fly while this one is scored
         if (fi + kPostWaves < kPostFiles && pos + kPostWaves < nn) {
             const int64_t pn1 = pos + kPostWaves;
-            prefetch_file(pn1, idx ? (int64_t)idx[pn1] : pn1, rows, w64, pb0, dense, tp, wfp, lenp, ccp, lane, pre);
+            prefetch_file(pn1, (int64_t)__builtin_amdgcn_readlane(tfile, fi + kPostWaves), rows, w64, pb0, dense, tp,
+                          wfp, lenp, ccp, lane, pre);
         }
 
         if (diag & 8) continue;

@@ -344,6 +344,29 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(OCC,
 //     as one f64 division and three coalesced stores per 64 files.
 constexpr float kLloScale = 0.499755859375f;   // 0.5 (1 - 2^-11): keys are in units of score / 400
 
+// Phase-skip diagnostics of v3 (tools/build_variant.sh -DPRUNE3_DIAG=n; results are wrong):
+// 1 skips the bound pass (template 0 is the only key), 2 skips exact scoring, 4 re-reads the
+// block's first row instead of streaming (no HBM traffic).
+#ifndef PRUNE3_DIAG
+#define PRUNE3_DIAG 0
+#endif
+// 8: per-wave s_memtime totals of v4's phases (dice_prune4), printed by prune_launch_match
+constexpr int kTPhases = 8;
+struct PhaseClock {
+    uint64_t acc[kTPhases];
+    uint64_t last;
+    __device__ __forceinline__ void init() {
+        for (int k = 0; k < kTPhases; ++k) acc[k] = 0;
+        last = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - last;
+        last = now;
+    }
+};
+#define PHASE(k) do { if (PRUNE3_DIAG & 8) pclk.mark(k); } while (0)
+
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -481,7 +504,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
         // the row is in LDS and counted before the next row's loads reuse its registers (else the
         // scheduler hoists those loads above the LDS writes: 24 row VGPRs live, spills at 64)
         __builtin_amdgcn_sched_barrier(0);
-        if (file + 1 < wend) prune_load<J, true>(nx, rows, file + 1, w64, wfp, lenp, ccp, lane);
+        if (file + 1 < wend) prune_load<J, true>(nx, rows, (PRUNE3_DIAG & 4) ? wbeg : file + 1, w64, wfp, lenp, ccp, lane);
 
         int32_t bi = -1, bd = 1;
         uint32_t bo = 0;
@@ -515,7 +538,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
             const uint32_t wf4 = 4u * wf;
             uint32_t key[TJ];
             uint32_t m1 = 0, m2 = 0;
-            if (!big && !ccf && wf >= wf_noclamp)
+            if (PRUNE3_DIAG & 1) {
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) key[j] = 0;
+                key[0] = m1 = lane == 0 ? 0x3F800001u : 0u;
+            } else if (!big && !ccf && wf >= wf_noclamp)
                 bound_pass3<TJ, false, false, false>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
             else if (!big && !ccf)
                 bound_pass3<TJ, false, false, true>(q8, stc, ccm, T, fb, negwv, m2big, lf, wf4, lane, key, m1, m2);
@@ -543,6 +570,10 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                     float llo = -1.0f;   // lower bound of best / 400 (f32); keys below it are dropped
                     int32_t l1;
                     const int32_t t1 = key_template(K1, m1, l1);
+                    if (PRUNE3_DIAG & 2) {
+                        bi = t1;
+                        bd = 1;
+                    } else {
                     const RecHead h1 = records_head(t1, soff, qrec, lane);   // in flight while K2 is found
                     score_template3(t1, h1, qrec, myrow, tcg, wf, lf, fast, lane, bi, bo, bd, llo);
                     // any other key still at or above the best score? (each lane's largest other
@@ -585,6 +616,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                                             lane, bi, bo, bd, llo);
                         }
                     }
+                    }   // PRUNE3_DIAG & 2
                 }
             }
         }
@@ -618,6 +650,349 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     }
 }
 
+
+// score_template3 for position-ordered tables: the order compare (later key wins ties) and the
+// result use the template index orig[ts].
+__device__ __forceinline__ void score_template4(int32_t ts, const RecHead& h, const uint4* __restrict__ qrec,
+                                                const uint64_t* myrow, const uint4* stc, const int32_t* sorig,
+                                                uint32_t wf, uint32_t lf, bool fast, int lane, int32_t& bi,
+                                                uint32_t& bo, int32_t& bd, float& llo) {
+    // constants and template index from LDS (uniform address: a broadcast read; a scalar load
+    // would share lgkmcnt with the row reads below and make them wait for it)
+    const uint4 c = stc[ts];
+    const int32_t to = (int32_t)rfl((uint32_t)sorig[ts]);
+    uint32_t acc = rec_bits(myrow, h.a) + rec_bits(myrow, h.b);   // zero records read word 0, mask 0
+    for (uint32_t r = h.r0 + 2 * kWave + lane; r < h.r1; r += 2 * kWave) {   // > 128 records
+        const uint4 a = qrec[r];
+        const uint4 b = r + kWave < h.r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+        acc += rec_bits(myrow, a) + rec_bits(myrow, b);
+    }
+    const uint32_t ov = rfl(__builtin_amdgcn_readlane(wave_incl_scan(acc), kWave - 1));
+    const int32_t den = den3(c, wf, lf);
+    const bool better = fast ? outranks_t<true>(to, ov, den, bi, bo, bd) : outranks_t<false>(to, ov, den, bi, bo, bd);
+    if (better) {
+        bi = to;
+        bo = ov;
+        bd = den;
+        llo = (float)bo * __builtin_amdgcn_rcpf((float)bd) * kLloScale;
+    }
+}
+
+// Row-only prefetch for v4 (the per-file scalars come per 64-file block, see dice_prune4).
+template <int J>
+__device__ __forceinline__ void row_load(uint64_t (&w)[J], const uint64_t* __restrict__ rows, int64_t file,
+                                         int32_t w64, int lane) {
+    const uint64_t* row = rows + file * w64;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        // w64 > 64 (J - 2): only the last two word slots can run past the row
+        const int32_t p = lane + j * kWave;
+        w[j] = j < J - 2 || p < w64 ? __builtin_nontemporal_load(row + p) : 0;
+    }
+}
+
+// ---- v4: slot-skipping (the default schedule) --------------------------------------------
+//
+// v3's per-pair bound, evaluated for few templates: the host sorts the templates by length
+// (content_normalized.length) into the 64-template lane slots, so each slot covers a narrow
+// length band, and keeps per slot {min length, max length, 4 min base - 3, max slack | max |Lf| << 16}.
+// For every template t of slot j and any file,
+//   D4_t = 4 base_t - 3 + 4 wf + max(|len_t - len_F| - slack_t, 0)
+//       >= 4 bmin_j - 3 + 4 wf + max(dist(len_F, [Lmin_j, Lmax_j]) - smax_j, 0) = D4_j
+//   m2_t <= 2 min(|Lf_t|, |W_F ∩ V|) <= 2 min(Mmax_j, wv)
+// so SB_j = 2 min(Mmax_j, wv) / D4_j bounds every key of slot j (lanes = slots: one vector pass
+// of ~13 VALU per file for all slots). Per file: the keys of the slot whose band holds len_F,
+// its top template scored exactly, then only the slots with SB_j >= the best score (2.7 of 10
+// on the config-3 files, numpy simulation over 4000 files: DESIGN.md) get per-template keys;
+// the rest is v3 (drop / score the largest remaining key / defer). Templates of skipped slots
+// score strictly below the best (SB_j, in f32 within 2^-21, < llo <= best (1 - 2^-11)).
+// Tables are in position (sorted) order; orig[] maps a position to the template index that
+// outputs and the tie rule (later key wins) use.
+struct Prune4Args {
+    const uint4* q8;       // [kTP] group bytes, by position
+    const uint4* tc;       // [kTP] v3 constants, by position
+    const uint32_t* ccm;   // [kTP] CC masks, by position
+    const uint32_t* qoff;  // [T + 1] record offsets, by position
+    const uint4* qrec;     // records, by position
+    const uint4* slot;     // [TJ] slot bounds {Lmin, Lmax, 4 bmin - 3, smax | Mmax << 16}
+    const int32_t* orig;   // [kTP] position -> template index
+    int32_t zkeep[2];      // last kept template index (file not / potential_false_positive?), -1 none
+    int32_t zpos[2];       // its position
+};
+
+template <bool BIG, bool CC, bool CLAMP>
+__device__ __forceinline__ uint32_t slot_key(const uint4* q8, const uint4* stc, const uint32_t* ccm, int32_t t,
+                                             uint32_t tag, int32_t T, bool pad, const uint32_t (&fb)[4],
+                                             uint32_t negwv, uint32_t m2big, uint32_t lf, uint32_t wf4) {
+    const uint4 c = stc[t];
+    uint32_t mm;
+    if (!BIG) {
+        const uint4 a = q8[t];
+        uint32_t d = __builtin_amdgcn_sad_u8(a.x, fb[0], negwv);
+        d = __builtin_amdgcn_sad_u8(a.y, fb[1], d);
+        d = __builtin_amdgcn_sad_u8(a.z, fb[2], d);
+        d = __builtin_amdgcn_sad_u8(a.w, fb[3], d);
+        mm = c.w - d;
+    } else {
+        mm = m2big;
+    }
+    const uint32_t x0 = __usad(c.x, lf, c.y);
+    const uint32_t x = CLAMP ? (uint32_t)max((int32_t)x0, 0) : x0;
+    const uint32_t d4 = c.z + wf4 + x;
+    const float q = (float)mm * __builtin_amdgcn_rcpf((float)d4);
+    uint32_t k = (__float_as_uint(q) & ~kKeyLow) | tag;
+    if (CC) k &= ~ccm[t];
+    if (pad) k = t < T ? k : 0u;
+    return k;
+}
+
+// Phases 1 and 2 of a file for one (BIG, CC, CLAMP) case: the keys of slot jstar, its top
+// template scored exactly, then the keys of every slot whose bound reaches the best score.
+// Returns with key[] filled (0 for skipped slots and the scored template) and llo / bi / bo / bd
+// set; first_scored false when slot jstar had no template with a nonzero bound.
+template <int TJ, bool BIG, bool CC, bool CLAMP>
+__device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, const uint32_t* ccm, const uint32_t* soff,
+                                            const int32_t* sorig, const Prune4Args& pa, const uint64_t* myrow, int32_t T, int32_t jstar,
+                                            uint32_t sbk, const uint32_t (&fb)[4], uint32_t negwv, uint32_t m2big,
+                                            uint32_t lf, uint32_t wf, uint32_t wf4, bool fast, int lane,
+                                            uint32_t (&key)[TJ], float& llo, int32_t& bi, uint32_t& bo, int32_t& bd,
+                                            PhaseClock& pclk) {
+    const int32_t t0 = lane + jstar * kWave;
+    uint32_t ks = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, t0, (uint32_t)(jstar + 1), T, (jstar + 1) * kWave > T, fb,
+                                           negwv, m2big, lf, wf4);
+    __builtin_amdgcn_wave_barrier();   // the row (written above) is read by other lanes below
+    const uint32_t K1 = rfl(__builtin_amdgcn_readlane(wave_incl_max(ks), kWave - 1));
+    PHASE(2);
+    if ((K1 & ~kKeyLow) != 0) {
+        int32_t l1;
+        const int32_t t1 = key_template(K1, ks, l1);
+        if (PRUNE3_DIAG & 2) {
+            bi = t1;
+            bd = 1;
+            llo = 1e30f;
+        } else {
+            score_template4(t1, records_head(t1, soff, pa.qrec, lane), pa.qrec, myrow, stc, sorig, wf, lf, fast,
+                            lane, bi, bo, bd, llo);
+        }
+        if (lane == l1) ks = 0;
+    }
+    PHASE(3);
+    // slots whose bound reaches the best score so far (every slot when nothing was scored)
+    const uint64_t mask = __ballot(lane < TJ && !(__uint_as_float(sbk) < llo));
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        if (j == jstar) key[j] = ks;
+        else if ((mask >> j) & 1)
+            key[j] = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, lane + j * kWave, (uint32_t)(j + 1), T,
+                                              j >= TJ - 2 && (j + 1) * kWave > T, fb, negwv, m2big, lf, wf4);
+        else key[j] = 0;
+    }
+    PHASE(4);
+}
+
+template <int J, int TJ, int NW>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_prune4(
+    const uint64_t* __restrict__ rows, int64_t n, int64_t per_wave, int32_t w64, int32_t T, Prune4Args pa,
+    const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
+    int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast,
+    bool zero_base, uint32_t wf_noclamp, int32_t* __restrict__ defer, uint32_t* __restrict__ ndefer,
+    int32_t max_evals, int32_t route_cands, uint64_t* __restrict__ diag_out) {
+    constexpr int kTP = TJ * kWave;
+    // LDS: [waves][J * 64] file rows | [kTP] uint4 group bytes | [kTP] uint4 constants | [kTP] cc
+    // masks | [T + 1] record offsets
+    extern __shared__ uint64_t lds[];
+    uint4* q8 = reinterpret_cast<uint4*>(lds + (size_t)NW * J * kWave);
+    uint4* stc = q8 + kTP;
+    uint32_t* ccm = reinterpret_cast<uint32_t*>(stc + kTP);
+    int32_t* sorig = reinterpret_cast<int32_t*>(ccm + kTP);
+    uint32_t* soff = reinterpret_cast<uint32_t*>(sorig + kTP);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    uint64_t* myrow = lds + (size_t)wave * J * kWave;
+    PhaseClock pclk;
+    if (PRUNE3_DIAG & 8) pclk.init();
+    for (int i = threadIdx.x; i < kTP; i += NW * kWave) {
+        q8[i] = pa.q8[i];
+        stc[i] = pa.tc[i];
+        ccm[i] = pa.ccm[i];
+        sorig[i] = pa.orig[i];
+    }
+    for (int i = threadIdx.x; i <= T; i += NW * kWave) soff[i] = pa.qoff[i];
+    const uint4 sb = lane < TJ ? pa.slot[lane] : make_uint4(0x7FFFFFFFu, 0, 0, 0);   // this lane's slot bound
+
+    const int64_t wbeg = ((int64_t)blockIdx.x * NW + wave) * per_wave;
+    const int64_t wend = min(n, wbeg + per_wave);
+    // per-file scalars by 64-file block: lane l holds file (block start + l), loaded one block ahead
+    // by vector loads and read per file with v_readlane. (Scalar loads of the next file's |W_F| /
+    // len_F share lgkmcnt with the LDS reads, whose waits then stalled on HBM latency every file.)
+    // (Loads are unconditional, at clamped indices: an exec-masked load merges with the register's
+    // old value, and the copy that merge needs makes the compiler wait for the load at once.)
+    uint32_t cwf = 0, cln = 0, ccc = 0, nwf = 0, nln = 0, ncc = 0;
+    uint64_t nw[J];
+    if (wbeg < wend) {
+        const int64_t f0 = min(wbeg + lane, n - 1);
+        nwf = wfp[f0];
+        nln = (uint32_t)lenp[f0];
+        ncc = ccp[f0];
+        row_load<J>(nw, rows, wbeg, w64, lane);
+    }
+    __syncthreads();
+
+    int32_t ri = -2, rd = 1;   // lane l: result of file (block start + l); -2 = none, -3 = deferred
+    uint32_t ro = 0;
+    if (PRUNE3_DIAG & 8) pclk.mark(7);
+    for (int64_t file = wbeg; file < wend; ++file) {   // wave-uniform
+        const int slot = (int)((file - wbeg) & (kWave - 1));
+        if (slot == 0) {   // this block's scalars (loaded a block ago); the next block's
+            cwf = nwf;
+            cln = nln;
+            ccc = ncc;
+            const int64_t nb = min(file + kWave + lane, n - 1);
+            nwf = wfp[nb];
+            nln = (uint32_t)lenp[nb];
+            ncc = ccp[nb];
+        }
+        uint32_t pc = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {   // the row buffer holds J * 64 words: no bounds test
+            myrow[lane + j * kWave] = nw[j];
+            pc += (uint32_t)__builtin_popcountll(nw[j]);
+        }
+        const uint32_t wf = rfl(__builtin_amdgcn_readlane(cwf, slot));
+        const int32_t lfi = (int32_t)rfl(__builtin_amdgcn_readlane(cln, slot));
+        const uint32_t lf = (uint32_t)lfi;
+        const bool ccf = __builtin_amdgcn_readlane(ccc, slot) != 0;
+        __builtin_amdgcn_sched_barrier(0);
+        PHASE(0);
+        row_load<J>(nw, rows, (PRUNE3_DIAG & 4) ? wbeg : min(file + 1, wend - 1), w64, lane);
+
+        int32_t bi = -1, bd = 1;
+        uint32_t bo = 0;
+        bool deferred = false;
+        if (lfi < 0 || wf >= (1u << 28) || (zero_base && wf == 0)) {
+            deferred = true;
+        } else {
+            const uint32_t pc0 = pc;
+            pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+            pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+            const bool big = __ballot(pc > 255u) != 0;
+            uint32_t fb[4] = {0, 0, 0, 0};
+            uint32_t negwv = 0, m2big = 0, wv;
+            if (!big) {
+                uint32_t x = pc << 24;
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x114, 0xf, 0xf, false) << 16;   // row_shr:4
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x118, 0xf, 0xf, false) << 8;    // row_shr:8
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x11C, 0xf, 0xf, false);         // row_shr:12
+#pragma unroll
+                for (int k = 0; k < 4; ++k) fb[k] = rfl(__builtin_amdgcn_readlane(x, 16 * k + 12));
+                wv = __builtin_amdgcn_sad_u8(fb[0], 0u, 0u);
+                wv = __builtin_amdgcn_sad_u8(fb[1], 0u, wv);
+                wv = __builtin_amdgcn_sad_u8(fb[2], 0u, wv);
+                wv = __builtin_amdgcn_sad_u8(fb[3], 0u, wv);
+                negwv = 0u - wv;
+            } else {
+                wv = rfl(__builtin_amdgcn_readlane(wave_incl_scan(pc0), kWave - 1));
+                m2big = 2u * wv;
+            }
+            if (wv == 0) {
+                // no vocabulary word: every kept template overlaps nothing and scores 0.0 (den >= 1);
+                // the later key wins the tie: the last kept template
+                bi = pa.zkeep[ccf ? 1 : 0];
+                if (bi >= 0) bd = den3(stc[pa.zpos[ccf ? 1 : 0]], wf, lf);
+            } else {
+                const uint32_t wf4 = 4u * wf;
+                // slot bounds, lanes = slots
+                const int32_t dist = max(max((int32_t)sb.x - lfi, lfi - (int32_t)sb.y), 0);
+                const uint32_t d4 = sb.z + wf4 + (uint32_t)max(dist - (int32_t)(sb.w & 0xFFFFu), 0);
+                const uint32_t mmx = 2u * min(sb.w >> 16, wv);
+                const uint32_t sbk = lane < TJ ? __float_as_uint((float)mmx * __builtin_amdgcn_rcpf((float)d4)) : 0u;
+                // the slot whose length band holds len_F (the last slot starting at or below it)
+                const uint64_t below = __ballot(lane < TJ && (int32_t)sb.x <= lfi);
+                const int32_t jstar = below ? 63 - (int32_t)__builtin_clzll(below) : 0;
+                const bool fast = corpus_fast && wf < (1u << 20) && lf < (1u << 21);
+                float llo = -1.0f;
+                uint32_t key[TJ];
+                PHASE(1);
+                if (!big && !ccf && wf >= wf_noclamp)
+                    prune4_keys<TJ, false, false, false>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                         lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                else if (!big && !ccf)
+                    prune4_keys<TJ, false, false, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                        lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                else if (!big)
+                    prune4_keys<TJ, false, true, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                       lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                else if (!ccf)
+                    prune4_keys<TJ, true, false, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                       lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                else
+                    prune4_keys<TJ, true, true, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                      lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                // the largest remaining key, scored while it can reach the best score
+                for (int32_t evals = 1;; ++evals) {
+                    uint32_t km = 0, live = 0;
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j) {
+                        if (__uint_as_float(key[j]) < llo) key[j] = 0;
+                        km = max(km, key[j]);
+                        if (evals == 2) live += (uint32_t)__builtin_popcountll(__ballot(key[j] != 0));
+                    }
+                    if (__ballot(km != 0) == 0) break;   // every template scored or dropped
+                    // a file whose bounds stay loose (it resembles several templates or none: stacked
+                    // licenses, long notices) goes to the postings kernels: after two exact scores
+                    // when more than route_cands templates can still reach the top, else after
+                    // max_evals
+                    if (evals == max_evals || (evals == 2 && (int32_t)live > route_cands)) {
+                        deferred = true;
+                        break;
+                    }
+                    const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
+                    int32_t ls;
+                    const int32_t ts = key_template(K, km, ls);
+                    if (lane == ls) {
+#pragma unroll
+                        for (int j = 0; j < TJ; ++j)
+                            if (j == (ts >> 6)) key[j] = 0;
+                    }
+                    score_template4(ts, records_head(ts, soff, pa.qrec, lane), pa.qrec, myrow, stc, sorig, wf,
+                                    lf, fast, lane, bi, bo, bd, llo);
+                }
+                PHASE(5);
+            }
+        }
+        if (deferred) bi = -3;
+        if (lane == slot) {
+            ri = bi;
+            ro = bo;
+            rd = bd;
+        }
+        if (slot == kWave - 1 || file + 1 == wend) {
+            const int64_t f = file - slot + lane;
+            const bool mine = lane <= slot;
+            if (mine && ri >= -1) {
+                const double s = ri >= 0 ? dice_score(ro, rd) : 0.0;
+                best_out[f] = (ri >= 0 && s >= thr) ? ri : -1;
+                ov_out[f] = ro;
+                score_out[f] = s;
+            }
+            const uint64_t dm = __ballot(mine && ri == -3);
+            if (dm) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(ndefer, (uint32_t)__builtin_popcountll(dm));
+                base = __builtin_amdgcn_readlane(base, 0);
+                if (mine && ri == -3) defer[base + lane_rank(dm)] = (int32_t)f;
+            }
+            ri = -2;
+        }
+        PHASE(6);
+    }
+    if ((PRUNE3_DIAG & 8) && diag_out && lane == 0) {
+        const int64_t gw = (int64_t)blockIdx.x * NW + wave;
+        for (int k = 0; k < kTPhases; ++k) diag_out[gw * (kTPhases + 1) + k] = pclk.acc[k];
+        diag_out[gw * (kTPhases + 1) + kTPhases] = (uint64_t)(wend > wbeg ? wend - wbeg : 0);
+    }
+}
+
 // ---- host side ---------------------------------------------------------------------------
 
 // the old schedules' padded template count (10 or 11 per lane), and v3's (ceil(T / 64) rounded
@@ -643,12 +1018,83 @@ static size_t prune3_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
 
 constexpr int32_t kRouteCands = 32;   // v3: candidates left after two exact scores above which a file is deferred
 
+// v4 tables: the templates in position order (stable sort by length), the per-slot bounds and
+// the position -> template map (dice_prune4).
+static int prune4_setup(dice_ctx* c, const dice_templates* t, const std::vector<uint32_t>& q8,
+                        const std::vector<uint4>& tc3, const std::vector<uint32_t>& cc3,
+                        const std::vector<uint32_t>& qoff, const std::vector<uint4>& qrec) {
+    const int32_t T = c->T;
+    const size_t tp = (size_t)kPruneMaxT;
+    std::vector<int32_t> pos2t((size_t)T);
+    for (int32_t i = 0; i < T; ++i) pos2t[(size_t)i] = i;
+    std::stable_sort(pos2t.begin(), pos2t.end(), [&](int32_t a, int32_t b) { return t->length[a] < t->length[b]; });
+    std::vector<uint32_t> q8p(tp * 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0);
+    std::vector<uint4> tcp(tp, make_uint4(0, 0, 0, 0)), recp;
+    std::vector<int32_t> orig(tp, -1);
+    recp.reserve(qrec.size());
+    for (int32_t p = 0; p < T; ++p) {
+        const int32_t i = pos2t[(size_t)p];
+        for (int k = 0; k < 4; ++k) q8p[(size_t)p * 4 + k] = q8[(size_t)i * 4 + k];
+        tcp[(size_t)p] = tc3[(size_t)i];
+        ccp[(size_t)p] = cc3[(size_t)i];
+        orig[(size_t)p] = i;
+        recp.insert(recp.end(), qrec.begin() + qoff[(size_t)i], qrec.begin() + qoff[(size_t)i + 1]);
+        offp[(size_t)p + 1] = (uint32_t)recp.size();
+    }
+    if (recp.empty()) recp.push_back(make_uint4(0, 0, 0, 0));
+    // slot bounds {Lmin, Lmax, 4 bmin - 3, smax | Mmax << 16}; an empty slot never holds len_F
+    // and bounds nothing (Mmax 0)
+    const int32_t nslot = prune3_tj(T);
+    std::vector<uint4> slot((size_t)nslot, make_uint4(0x7FFFFFFFu, 0x7FFFFFFFu, 0, 0));
+    for (int32_t j = 0; j < nslot; ++j) {
+        int64_t lmin = INT64_MAX, lmax = 0, bmin = INT64_MAX, smax = 0, mmax = 0;
+        for (int32_t p = j * kWave; p < std::min(T, (j + 1) * kWave); ++p) {
+            const int32_t i = pos2t[(size_t)p];
+            lmin = std::min<int64_t>(lmin, t->length[i]);
+            lmax = std::max<int64_t>(lmax, t->length[i]);
+            bmin = std::min<int64_t>(bmin, (int64_t)t->lf_size[i] - (int64_t)t->fields_set_size[i]);
+            smax = std::max<int64_t>(smax, std::max(t->length_slack[i], 0));
+            mmax = std::max<int64_t>(mmax, t->lf_size[i]);
+        }
+        if (lmin == INT64_MAX) continue;
+        // post_feasible: |Lf| < 65535, slack <= 32767
+        slot[(size_t)j] = make_uint4((uint32_t)lmin, (uint32_t)lmax, (uint32_t)(4 * bmin - 3),
+                                     (uint32_t)smax | ((uint32_t)mmax << 16));
+    }
+    // the last kept template (the tie winner when every score is 0.0) for unflagged / CC-flagged files
+    int32_t zk[2] = {-1, -1}, zp[2] = {-1, -1};
+    for (int32_t p = 0; p < T; ++p) {
+        const int32_t i = pos2t[(size_t)p];
+        if (i > zk[0]) zk[0] = i, zp[0] = p;
+        if (!t->is_cc[i] && i > zk[1]) zk[1] = i, zp[1] = p;
+    }
+    int rc;
+    if ((rc = dalloc_bytes(&c->d_p4q8, q8p.size() * 4)) || (rc = dalloc_bytes(&c->d_p4tc, tcp.size() * 16)) ||
+        (rc = dalloc_bytes(&c->d_p4cc, ccp.size() * 4)) || (rc = dalloc_bytes(&c->d_p4off, offp.size() * 4)) ||
+        (rc = dalloc_bytes(&c->d_p4rec, recp.size() * 16)) || (rc = dalloc_bytes(&c->d_p4slot, slot.size() * 16)) ||
+        (rc = dalloc_bytes(&c->d_p4orig, orig.size() * 4)))
+        return rc;
+    if (hipMemcpy(c->d_p4q8, q8p.data(), q8p.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4tc, tcp.data(), tcp.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4cc, ccp.data(), ccp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4off, offp.data(), offp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4rec, recp.data(), recp.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4slot, slot.data(), slot.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4orig, orig.data(), orig.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(DICE_E_DEVICE, "pruned-match v4 plan upload failed");
+    for (int k = 0; k < 2; ++k) {
+        c->p4_zkeep[k] = zk[k];
+        c->p4_zpos[k] = zp[k] < 0 ? 0 : zp[k];
+    }
+    return DICE_OK;
+}
+
 int prune_setup(dice_ctx* c, const dice_templates* t) {
     const char* e = getenv("DICE_POST_PRUNE");
     if (e && *e == '0') return DICE_OK;
     const int32_t T = c->T, w64 = c->w64;
     if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024 ||
-        prune3_lds_bytes(kPruneWaves, w64, T) > 160 * 1024)
+        prune3_lds_bytes(kPruneWaves, w64, T) + (size_t)prune3_tj(T) * kWave * 4 > 160 * 1024)
         return DICE_OK;
     // every table padded to the largest template count (704): each schedule reads its prefix.
     // Group counts A_g = |Lf_t ∩ g| clamped to bytes; the old and the v3 constants; the v3 CC
@@ -720,6 +1166,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
         c->n_cu = 256;
+    if ((rc = prune4_setup(c, t, q8, tc3, cc3, qoff, qrec))) return rc;
     c->prune = true;
     return DICE_OK;
 }
@@ -779,8 +1226,69 @@ static int launch_prune3(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) 
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune3 launch failed");
 }
 
+template <int J, int TJ>
+static int launch_prune4(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    constexpr int NW = kPruneWaves;
+    const size_t lds = prune3_lds_bytes(NW, c->w64, c->T) + (size_t)prune3_tj(c->T) * kWave * 4;   // + orig map
+    auto kern = dice_prune4<J, TJ, NW>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / NW, (160 * 1024) / (int64_t)lds));
+    const int64_t max_waves = per_cu * c->n_cu * NW;
+    const int64_t per_wave = std::max<int64_t>(1, (b->n + max_waves - 1) / max_waves);
+    const int64_t groups = ((b->n + per_wave - 1) / per_wave + NW - 1) / NW;
+    const int32_t max_evals = c->prune_max_evals == 0 ? INT32_MAX : c->prune_max_evals;
+    const int32_t route = c->prune_max_evals == 0 ? INT32_MAX : c->prune_route;
+    Prune4Args pa;
+    pa.q8 = (const uint4*)c->d_p4q8;
+    pa.tc = (const uint4*)c->d_p4tc;
+    pa.ccm = (const uint32_t*)c->d_p4cc;
+    pa.qoff = (const uint32_t*)c->d_p4off;
+    pa.qrec = (const uint4*)c->d_p4rec;
+    pa.slot = (const uint4*)c->d_p4slot;
+    pa.orig = (const int32_t*)c->d_p4orig;
+    for (int k = 0; k < 2; ++k) {
+        pa.zkeep[k] = c->p4_zkeep[k];
+        pa.zpos[k] = c->p4_zpos[k];
+    }
+    uint64_t* diag = nullptr;
+    if (PRUNE3_DIAG & 8) {
+        static uint64_t* dbuf = nullptr;
+        if (!dbuf && hipMalloc(&dbuf, (size_t)groups * NW * (kTPhases + 1) * 8) != hipSuccess) dbuf = nullptr;
+        diag = dbuf;
+        if (diag) (void)hipMemsetAsync(diag, 0, (size_t)groups * NW * (kTPhases + 1) * 8, s);
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows, b->n,
+                       per_wave, c->w64, c->T, pa, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score,
+                       c->post_fast, c->prune_zero_base, c->prune_wf_noclamp, b->d_defer, b->d_ndefer, max_evals,
+                       route, diag);
+    if ((PRUNE3_DIAG & 8) && diag) {
+        // diagnostic build only: per-phase shader-clock totals over all waves, per file
+        std::vector<uint64_t> h((size_t)groups * NW * (kTPhases + 1));
+        (void)hipMemcpyAsync(h.data(), diag, h.size() * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        double tot[kTPhases + 1] = {0};
+        for (size_t w = 0; w < (size_t)groups * NW; ++w)
+            for (int k = 0; k <= kTPhases; ++k) tot[k] += (double)h[w * (kTPhases + 1) + k];
+        fprintf(stderr, "[prune4 phases] cycles/file:");
+        for (int k = 0; k < kTPhases; ++k) fprintf(stderr, " p%d=%.0f", k, tot[k] / std::max(1.0, tot[kTPhases]));
+        fprintf(stderr, "  (files %.0f)\n", tot[kTPhases]);
+    }
+    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune4 launch failed");
+}
+
 template <int J>
 static int launch_prune3_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+    if (c->prune_sched != 6) {   // v4 unless v3 is asked for (A/B)
+        switch (prune3_tj(c->T)) {
+            case 2: return launch_prune4<J, 2>(c, b, thr, s);
+            case 4: return launch_prune4<J, 4>(c, b, thr, s);
+            case 6: return launch_prune4<J, 6>(c, b, thr, s);
+            case 8: return launch_prune4<J, 8>(c, b, thr, s);
+            case 10: return launch_prune4<J, 10>(c, b, thr, s);
+            default: return launch_prune4<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
+        }
+    }
     switch (prune3_tj(c->T)) {
         case 2: return launch_prune3<J, 2>(c, b, thr, s);
         case 4: return launch_prune3<J, 4>(c, b, thr, s);

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build liblicensee_dice.so with extra compile flags into licensee_amd/lib/var/<name>.so, for
+# A/B runs of compile-time kernel variants on the GPU box (LICENSEE_DICE_LIB=<path>).
+#   tools/build_variant.sh <name> [-DFLAG=...]...
+set -e
+NAME=$1; shift
+cd "$(dirname "$0")/.."
+mkdir -p licensee_amd/lib/var
+C=licensee_amd/csrc
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall "$@" -o licensee_amd/lib/var/$NAME.so \
+  $C/dice.hip $C/dice_lds.hip $C/dice_post.hip $C/dice_prune.hip $C/dice_program.cpp $C/dice_shard.cpp -lhiprtc
+echo licensee_amd/lib/var/$NAME.so
