@@ -651,16 +651,30 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 }
 
 
+// records_head for v4: one LDS read of srec[ts], srec[ts + 1] (template index | record offset
+// << 10) gives the record range and the template index at once.
+__device__ __forceinline__ RecHead records_head4(int32_t ts, const uint32_t* srec, const uint4* __restrict__ qrec,
+                                                 int lane, int32_t& to) {
+    RecHead h;
+    const uint32_t e0 = rfl(srec[ts]), e1 = rfl(srec[ts + 1]);
+    to = (int32_t)(e0 & 1023u);
+    h.r0 = e0 >> 10;
+    h.r1 = e1 >> 10;
+    const uint32_t r = h.r0 + lane;
+    h.a = r < h.r1 ? qrec[r] : make_uint4(0, 0, 0, 0);
+    h.b = r + kWave < h.r1 ? qrec[r + kWave] : make_uint4(0, 0, 0, 0);
+    return h;
+}
+
 // score_template3 for position-ordered tables: the order compare (later key wins ties) and the
-// result use the template index orig[ts].
-__device__ __forceinline__ void score_template4(int32_t ts, const RecHead& h, const uint4* __restrict__ qrec,
-                                                const uint64_t* myrow, const uint4* stc, const int32_t* sorig,
+// result use the template index `to`.
+__device__ __forceinline__ void score_template4(int32_t ts, int32_t to, const RecHead& h, const uint4* __restrict__ qrec,
+                                                const uint64_t* myrow, const uint4* stc,
                                                 uint32_t wf, uint32_t lf, bool fast, int lane, int32_t& bi,
                                                 uint32_t& bo, int32_t& bd, float& llo) {
-    // constants and template index from LDS (uniform address: a broadcast read; a scalar load
-    // would share lgkmcnt with the row reads below and make them wait for it)
+    // constants from LDS (uniform address: a broadcast read; a scalar load would share lgkmcnt
+    // with the row reads below and make them wait for it)
     const uint4 c = stc[ts];
-    const int32_t to = (int32_t)rfl((uint32_t)sorig[ts]);
     uint32_t acc = rec_bits(myrow, h.a) + rec_bits(myrow, h.b);   // zero records read word 0, mask 0
     for (uint32_t r = h.r0 + 2 * kWave + lane; r < h.r1; r += 2 * kWave) {   // > 128 records
         const uint4 a = qrec[r];
@@ -678,16 +692,54 @@ __device__ __forceinline__ void score_template4(int32_t ts, const RecHead& h, co
     }
 }
 
-// Row-only prefetch for v4 (the per-file scalars come per 64-file block, see dice_prune4).
-template <int J>
-__device__ __forceinline__ void row_load(uint64_t (&w)[J], const uint64_t* __restrict__ rows, int64_t file,
+// Row-only prefetch for v4 (the per-file scalars come per 64-file block, see dice_prune4): J2
+// 16-byte loads per lane, lane l of load j holding words 2q, 2q + 1 of q = l + 64 j (a 1 KiB
+// coalesced global_load_dwordx4 per wave instruction; rows are 16-byte aligned when w64 is
+// even, which the host checks). The bound's word groups follow the layout: word p is in group
+// ((p / 2) mod 64) / 4, so a lane's words sit in one group and group g is lanes 4g..4g+3.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// P4_ROW16 (A/B): 1 = 16-byte row loads, word groups ((w / 2) mod 64) / 4; 0 = 8-byte loads (two
+// per uint4: words l + 128 j and l + 64 + 128 j of lane l), word groups (w mod 64) / 4
+#ifndef P4_ROW16
+#define P4_ROW16 0   // 16-byte loads measured 1.30 vs 0.98 ms (2 interleaved reps, one box): 8-byte
+#endif
+
+template <int J2>
+__device__ __forceinline__ void row_load(uint4 (&w)[J2], const uint64_t* __restrict__ rows, int64_t file,
                                          int32_t w64, int lane) {
+#if P4_ROW16
+    const u32x4* row = reinterpret_cast<const u32x4*>(rows + file * w64);
+    const int32_t w128 = w64 >> 1;
+#pragma unroll
+    for (int j = 0; j < J2; ++j) {
+        const int32_t q = lane + j * kWave;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (q < w128) v = __builtin_nontemporal_load(row + q);
+        w[j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+#else
     const uint64_t* row = rows + file * w64;
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        // w64 > 64 (J - 2): only the last two word slots can run past the row
-        const int32_t p = lane + j * kWave;
-        w[j] = j < J - 2 || p < w64 ? __builtin_nontemporal_load(row + p) : 0;
+    for (int j = 0; j < J2; ++j) {
+        const int32_t p0 = lane + 2 * j * kWave, p1 = p0 + kWave;
+        const uint64_t a = p0 < w64 ? __builtin_nontemporal_load(row + p0) : 0;
+        const uint64_t b = p1 < w64 ? __builtin_nontemporal_load(row + p1) : 0;
+        w[j] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+#endif
+}
+
+template <int J2>
+__device__ __forceinline__ void row_store(uint64_t* myrow, const uint4 (&w)[J2], int lane) {
+#pragma unroll
+    for (int j = 0; j < J2; ++j) {
+#if P4_ROW16
+        reinterpret_cast<uint4*>(myrow)[lane + j * kWave] = w[j];
+#else
+        myrow[lane + 2 * j * kWave] = (uint64_t)w[j].x | ((uint64_t)w[j].y << 32);
+        myrow[lane + (2 * j + 1) * kWave] = (uint64_t)w[j].z | ((uint64_t)w[j].w << 32);
+#endif
     }
 }
 
@@ -712,10 +764,9 @@ struct Prune4Args {
     const uint4* q8;       // [kTP] group bytes, by position
     const uint4* tc;       // [kTP] v3 constants, by position
     const uint32_t* ccm;   // [kTP] CC masks, by position
-    const uint32_t* qoff;  // [T + 1] record offsets, by position
+    const uint32_t* srec;  // [kTP + 1] template index | record offset << 10, by position
     const uint4* qrec;     // records, by position
     const uint4* slot;     // [TJ] slot bounds {Lmin, Lmax, 4 bmin - 3, smax | Mmax << 16}
-    const int32_t* orig;   // [kTP] position -> template index
     int32_t zkeep[2];      // last kept template index (file not / potential_false_positive?), -1 none
     int32_t zpos[2];       // its position
 };
@@ -751,12 +802,12 @@ __device__ __forceinline__ uint32_t slot_key(const uint4* q8, const uint4* stc, 
 // Returns with key[] filled (0 for skipped slots and the scored template) and llo / bi / bo / bd
 // set; first_scored false when slot jstar had no template with a nonzero bound.
 template <int TJ, bool BIG, bool CC, bool CLAMP>
-__device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, const uint32_t* ccm, const uint32_t* soff,
-                                            const int32_t* sorig, const Prune4Args& pa, const uint64_t* myrow, int32_t T, int32_t jstar,
+__device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, const uint32_t* ccm, const uint32_t* srec,
+                                            const Prune4Args& pa, const uint64_t* myrow, int32_t T, int32_t jstar,
                                             uint32_t sbk, const uint32_t (&fb)[4], uint32_t negwv, uint32_t m2big,
                                             uint32_t lf, uint32_t wf, uint32_t wf4, bool fast, int lane,
-                                            uint32_t (&key)[TJ], float& llo, int32_t& bi, uint32_t& bo, int32_t& bd,
-                                            PhaseClock& pclk) {
+                                            uint32_t (&key)[TJ], uint32_t& lane_max, float& llo, int32_t& bi,
+                                            uint32_t& bo, int32_t& bd, PhaseClock& pclk) {
     const int32_t t0 = lane + jstar * kWave;
     uint32_t ks = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, t0, (uint32_t)(jstar + 1), T, (jstar + 1) * kWave > T, fb,
                                            negwv, m2big, lf, wf4);
@@ -771,14 +822,16 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
             bd = 1;
             llo = 1e30f;
         } else {
-            score_template4(t1, records_head(t1, soff, pa.qrec, lane), pa.qrec, myrow, stc, sorig, wf, lf, fast,
-                            lane, bi, bo, bd, llo);
+            int32_t to;
+            const RecHead h = records_head4(t1, srec, pa.qrec, lane, to);
+            score_template4(t1, to, h, pa.qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
         }
         if (lane == l1) ks = 0;
     }
     PHASE(3);
     // slots whose bound reaches the best score so far (every slot when nothing was scored)
     const uint64_t mask = __ballot(lane < TJ && !(__uint_as_float(sbk) < llo));
+    lane_max = 0;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
         if (j == jstar) key[j] = ks;
@@ -786,6 +839,7 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
             key[j] = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, lane + j * kWave, (uint32_t)(j + 1), T,
                                               j >= TJ - 2 && (j + 1) * kWave > T, fb, negwv, m2big, lf, wf4);
         else key[j] = 0;
+        lane_max = max(lane_max, key[j]);
     }
     PHASE(4);
 }
@@ -798,27 +852,29 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     bool zero_base, uint32_t wf_noclamp, int32_t* __restrict__ defer, uint32_t* __restrict__ ndefer,
     int32_t max_evals, int32_t route_cands, uint64_t* __restrict__ diag_out) {
     constexpr int kTP = TJ * kWave;
-    // LDS: [waves][J * 64] file rows | [kTP] uint4 group bytes | [kTP] uint4 constants | [kTP] cc
-    // masks | [T + 1] record offsets
+    // LDS: the tables first (their per-slot addresses then fit the 16-bit instruction offsets: no
+    // address registers per slot) -- [kTP] uint4 group bytes | [kTP] uint4 constants | [kTP] cc
+    // masks | [64] slot bounds | [kTP + 1] template index | record offset << 10 -- then the
+    // waves' rows of J2 * 128 words
     extern __shared__ uint64_t lds[];
-    uint4* q8 = reinterpret_cast<uint4*>(lds + (size_t)NW * J * kWave);
+    uint4* q8 = reinterpret_cast<uint4*>(lds);
     uint4* stc = q8 + kTP;
     uint32_t* ccm = reinterpret_cast<uint32_t*>(stc + kTP);
-    int32_t* sorig = reinterpret_cast<int32_t*>(ccm + kTP);
-    uint32_t* soff = reinterpret_cast<uint32_t*>(sorig + kTP);
+    uint4* ssb = reinterpret_cast<uint4*>(ccm + kTP);   // lanes >= TJ: empty slots
+    uint32_t* srec = reinterpret_cast<uint32_t*>(ssb + kWave);
+    uint64_t* rows0 = lds + (((size_t)kTP * 36 + kWave * 16 + ((size_t)kTP + 1) * 4 + 15) / 16) * 2;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
-    uint64_t* myrow = lds + (size_t)wave * J * kWave;
+    uint64_t* myrow = rows0 + (size_t)wave * ((J + 1) / 2) * 2 * kWave;
     PhaseClock pclk;
     if (PRUNE3_DIAG & 8) pclk.init();
     for (int i = threadIdx.x; i < kTP; i += NW * kWave) {
         q8[i] = pa.q8[i];
         stc[i] = pa.tc[i];
         ccm[i] = pa.ccm[i];
-        sorig[i] = pa.orig[i];
     }
-    for (int i = threadIdx.x; i <= T; i += NW * kWave) soff[i] = pa.qoff[i];
-    const uint4 sb = lane < TJ ? pa.slot[lane] : make_uint4(0x7FFFFFFFu, 0, 0, 0);   // this lane's slot bound
+    for (int i = threadIdx.x; i <= kTP; i += NW * kWave) srec[i] = pa.srec[i];
+    if (threadIdx.x < kWave) ssb[threadIdx.x] = threadIdx.x < TJ ? pa.slot[threadIdx.x] : make_uint4(0x7FFFFFFFu, 0, 0, 0);
 
     const int64_t wbeg = ((int64_t)blockIdx.x * NW + wave) * per_wave;
     const int64_t wend = min(n, wbeg + per_wave);
@@ -827,14 +883,23 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     // len_F share lgkmcnt with the LDS reads, whose waits then stalled on HBM latency every file.)
     // (Loads are unconditional, at clamped indices: an exec-masked load merges with the register's
     // old value, and the copy that merge needs makes the compiler wait for the load at once.)
-    uint32_t cwf = 0, cln = 0, ccc = 0, nwf = 0, nln = 0, ncc = 0;
-    uint64_t nw[J];
+    // cwf = min(|W_F|, 2^28) | cc << 31 (|W_F| >= 2^28 defers the file either way) and cln = len_F
+    // of the current block; the next block's raw values (nwf, nln, ncc) are loaded at the block's
+    // first file and packed at its last, long after they arrived.
+    uint32_t cwf = 0, cln = 0, nwf = 0, nln = 0, ncc = 0;
+    constexpr int J2 = (J + 1) / 2;
+    uint32_t pc = 0;   // the current row's bit count per lane
     if (wbeg < wend) {
         const int64_t f0 = min(wbeg + lane, n - 1);
-        nwf = wfp[f0];
-        nln = (uint32_t)lenp[f0];
-        ncc = ccp[f0];
-        row_load<J>(nw, rows, wbeg, w64, lane);
+        cwf = min(wfp[f0], 1u << 28) | ((uint32_t)(ccp[f0] != 0) << 31);
+        cln = (uint32_t)lenp[f0];
+        uint4 w0[J2];
+        row_load<J2>(w0, rows, wbeg, w64, lane);
+        row_store<J2>(myrow, w0, lane);   // the row buffer holds J2 * 128 words: no bounds test
+#pragma unroll
+        for (int j = 0; j < J2; ++j)
+            pc += (uint32_t)__builtin_popcount(w0[j].x) + (uint32_t)__builtin_popcount(w0[j].y) +
+                  (uint32_t)__builtin_popcount(w0[j].z) + (uint32_t)__builtin_popcount(w0[j].w);
     }
     __syncthreads();
 
@@ -843,28 +908,22 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     if (PRUNE3_DIAG & 8) pclk.mark(7);
     for (int64_t file = wbeg; file < wend; ++file) {   // wave-uniform
         const int slot = (int)((file - wbeg) & (kWave - 1));
-        if (slot == 0) {   // this block's scalars (loaded a block ago); the next block's
-            cwf = nwf;
-            cln = nln;
-            ccc = ncc;
+        if (slot == 0) {   // the next block's scalars
             const int64_t nb = min(file + kWave + lane, n - 1);
             nwf = wfp[nb];
             nln = (uint32_t)lenp[nb];
             ncc = ccp[nb];
         }
-        uint32_t pc = 0;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {   // the row buffer holds J * 64 words: no bounds test
-            myrow[lane + j * kWave] = nw[j];
-            pc += (uint32_t)__builtin_popcountll(nw[j]);
-        }
-        const uint32_t wf = rfl(__builtin_amdgcn_readlane(cwf, slot));
+        // the next file's row: loaded now, written to the LDS row buffer at the end of this file
+        // (registers consumed in the iteration that loads them: no copies, no early wait)
+        uint4 nw[J2];
+        row_load<J2>(nw, rows, (PRUNE3_DIAG & 4) ? wbeg : min(file + 1, wend - 1), w64, lane);
+        const uint32_t wfx = rfl(__builtin_amdgcn_readlane(cwf, slot));
+        const uint32_t wf = wfx & 0x7FFFFFFFu;
+        const bool ccf = (wfx >> 31) != 0;
         const int32_t lfi = (int32_t)rfl(__builtin_amdgcn_readlane(cln, slot));
         const uint32_t lf = (uint32_t)lfi;
-        const bool ccf = __builtin_amdgcn_readlane(ccc, slot) != 0;
-        __builtin_amdgcn_sched_barrier(0);
         PHASE(0);
-        row_load<J>(nw, rows, (PRUNE3_DIAG & 4) ? wbeg : min(file + 1, wend - 1), w64, lane);
 
         int32_t bi = -1, bd = 1;
         uint32_t bo = 0;
@@ -902,6 +961,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
             } else {
                 const uint32_t wf4 = 4u * wf;
                 // slot bounds, lanes = slots
+                const uint4 sb = ssb[lane];
                 const int32_t dist = max(max((int32_t)sb.x - lfi, lfi - (int32_t)sb.y), 0);
                 const uint32_t d4 = sb.z + wf4 + (uint32_t)max(dist - (int32_t)(sb.w & 0xFFFFu), 0);
                 const uint32_t mmx = 2u * min(sb.w >> 16, wv);
@@ -911,24 +971,26 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                 const int32_t jstar = below ? 63 - (int32_t)__builtin_clzll(below) : 0;
                 const bool fast = corpus_fast && wf < (1u << 20) && lf < (1u << 21);
                 float llo = -1.0f;
-                uint32_t key[TJ];
+                uint32_t key[TJ], lmax;
                 PHASE(1);
                 if (!big && !ccf && wf >= wf_noclamp)
-                    prune4_keys<TJ, false, false, false>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                         lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                    prune4_keys<TJ, false, false, false>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                         lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else if (!big && !ccf)
-                    prune4_keys<TJ, false, false, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                        lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                    prune4_keys<TJ, false, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                        lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else if (!big)
-                    prune4_keys<TJ, false, true, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                       lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                    prune4_keys<TJ, false, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else if (!ccf)
-                    prune4_keys<TJ, true, false, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                       lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
+                    prune4_keys<TJ, true, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else
-                    prune4_keys<TJ, true, true, true>(q8, stc, ccm, soff, sorig, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                      lf, wf, wf4, fast, lane, key, llo, bi, bo, bd, pclk);
-                // the largest remaining key, scored while it can reach the best score
+                    prune4_keys<TJ, true, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                                                      lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
+                // the largest remaining key, scored while it can reach the best score (most files:
+                // no key is left at or above the best score, one compare per lane)
+                if (__ballot(lmax != 0 && !(__uint_as_float(lmax) < llo)) != 0)
                 for (int32_t evals = 1;; ++evals) {
                     uint32_t km = 0, live = 0;
 #pragma unroll
@@ -954,8 +1016,9 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                         for (int j = 0; j < TJ; ++j)
                             if (j == (ts >> 6)) key[j] = 0;
                     }
-                    score_template4(ts, records_head(ts, soff, pa.qrec, lane), pa.qrec, myrow, stc, sorig, wf,
-                                    lf, fast, lane, bi, bo, bd, llo);
+                    int32_t to;
+                    const RecHead h = records_head4(ts, srec, pa.qrec, lane, to);
+                    score_template4(ts, to, h, pa.qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
                 }
                 PHASE(5);
             }
@@ -984,6 +1047,18 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
             }
             ri = -2;
         }
+        if (slot == kWave - 1) {   // the next block's scalars, packed (they arrived long ago)
+            cwf = min(nwf, 1u << 28) | ((uint32_t)(ncc != 0) << 31);
+            cln = nln;
+        }
+        // the next file's row into the LDS buffer (LDS ops of a wave run in order: this file's
+        // reads of its row are done) and its bit counts
+        pc = 0;
+        row_store<J2>(myrow, nw, lane);
+#pragma unroll
+        for (int j = 0; j < J2; ++j)
+            pc += (uint32_t)__builtin_popcount(nw[j].x) + (uint32_t)__builtin_popcount(nw[j].y) +
+                  (uint32_t)__builtin_popcount(nw[j].z) + (uint32_t)__builtin_popcount(nw[j].w);
         PHASE(6);
     }
     if ((PRUNE3_DIAG & 8) && diag_out && lane == 0) {
@@ -1011,6 +1086,12 @@ static int32_t prune3_j(int32_t w64) {
     const int32_t jw = (w64 + kWave - 1) / kWave;
     return jw <= 2 ? jw : jw <= 4 ? 4 : jw <= 6 ? 6 : 8;
 }
+// v4: rows of ((J + 1) / 2) * 128 words, the v3 tables and the position -> template map
+static size_t prune4_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
+    const size_t tp = (size_t)prune3_tj(T) * kWave;
+    return (size_t)nw * ((prune3_j(w64) + 1) / 2) * 2 * kWave * 8 +
+           (tp * (16 + 16 + 4) + kWave * 16 + (tp + 1) * 4 + 15) / 16 * 16;
+}
 static size_t prune3_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
     const size_t tp = (size_t)prune3_tj(T) * kWave;
     return (size_t)nw * prune3_j(w64) * kWave * 8 + tp * (16 + 16 + 4) + ((size_t)T + 1) * 4;
@@ -1028,18 +1109,34 @@ static int prune4_setup(dice_ctx* c, const dice_templates* t, const std::vector<
     std::vector<int32_t> pos2t((size_t)T);
     for (int32_t i = 0; i < T; ++i) pos2t[(size_t)i] = i;
     std::stable_sort(pos2t.begin(), pos2t.end(), [&](int32_t a, int32_t b) { return t->length[a] < t->length[b]; });
-    std::vector<uint32_t> q8p(tp * 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0);
+    std::vector<uint32_t> q8p(tp * 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0), srec(tp + 1, 0);
     std::vector<uint4> tcp(tp, make_uint4(0, 0, 0, 0)), recp;
-    std::vector<int32_t> orig(tp, -1);
     recp.reserve(qrec.size());
+    const int32_t w64 = c->w64;
     for (int32_t p = 0; p < T; ++p) {
         const int32_t i = pos2t[(size_t)p];
-        for (int k = 0; k < 4; ++k) q8p[(size_t)p * 4 + k] = q8[(size_t)i * 4 + k];
+        // group counts in v4's word groups: word w in group ((w / 2) mod 64) / 4 (16-byte row loads)
+        uint32_t gc[kPruneGroups] = {0};
+        const uint64_t* r = t->lf_bits + (size_t)i * w64;
+        for (int32_t w = 0; w < w64; ++w)
+            gc[((P4_ROW16 ? w >> 1 : w) % kWave) / (kWave / kPruneGroups)] += (uint32_t)__builtin_popcountll(r[w]);
+        uint32_t sum8 = 0;
+        for (int g = 0; g < kPruneGroups; ++g) {
+            const uint32_t a8 = std::min<uint32_t>(gc[g], 255u);
+            sum8 += a8;
+            q8p[(size_t)p * 4 + g / 4] |= a8 << (8 * (g % 4));
+        }
         tcp[(size_t)p] = tc3[(size_t)i];
+        tcp[(size_t)p].w = sum8;
         ccp[(size_t)p] = cc3[(size_t)i];
-        orig[(size_t)p] = i;
         recp.insert(recp.end(), qrec.begin() + qoff[(size_t)i], qrec.begin() + qoff[(size_t)i + 1]);
         offp[(size_t)p + 1] = (uint32_t)recp.size();
+    }
+    // template index | record offset << 10 per position (padding positions: empty ranges)
+    if (recp.size() >= (1u << 22)) return fail(DICE_E_ARG, "too many template records for the pruned match");
+    for (size_t p = 0; p <= tp; ++p) {
+        const uint32_t off = offp[std::min<size_t>(p, (size_t)T)];
+        srec[p] = (p < (size_t)T ? (uint32_t)pos2t[p] : 0u) | (off << 10);
     }
     if (recp.empty()) recp.push_back(make_uint4(0, 0, 0, 0));
     // slot bounds {Lmin, Lmax, 4 bmin - 3, smax | Mmax << 16}; an empty slot never holds len_F
@@ -1070,17 +1167,15 @@ static int prune4_setup(dice_ctx* c, const dice_templates* t, const std::vector<
     }
     int rc;
     if ((rc = dalloc_bytes(&c->d_p4q8, q8p.size() * 4)) || (rc = dalloc_bytes(&c->d_p4tc, tcp.size() * 16)) ||
-        (rc = dalloc_bytes(&c->d_p4cc, ccp.size() * 4)) || (rc = dalloc_bytes(&c->d_p4off, offp.size() * 4)) ||
-        (rc = dalloc_bytes(&c->d_p4rec, recp.size() * 16)) || (rc = dalloc_bytes(&c->d_p4slot, slot.size() * 16)) ||
-        (rc = dalloc_bytes(&c->d_p4orig, orig.size() * 4)))
+        (rc = dalloc_bytes(&c->d_p4cc, ccp.size() * 4)) || (rc = dalloc_bytes(&c->d_p4off, srec.size() * 4)) ||
+        (rc = dalloc_bytes(&c->d_p4rec, recp.size() * 16)) || (rc = dalloc_bytes(&c->d_p4slot, slot.size() * 16)))
         return rc;
     if (hipMemcpy(c->d_p4q8, q8p.data(), q8p.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_p4tc, tcp.data(), tcp.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_p4cc, ccp.data(), ccp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_p4off, offp.data(), offp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_p4off, srec.data(), srec.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_p4rec, recp.data(), recp.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_p4slot, slot.data(), slot.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_p4orig, orig.data(), orig.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(c->d_p4slot, slot.data(), slot.size() * 16, hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "pruned-match v4 plan upload failed");
     for (int k = 0; k < 2; ++k) {
         c->p4_zkeep[k] = zk[k];
@@ -1094,7 +1189,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     if (e && *e == '0') return DICE_OK;
     const int32_t T = c->T, w64 = c->w64;
     if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024 ||
-        prune3_lds_bytes(kPruneWaves, w64, T) + (size_t)prune3_tj(T) * kWave * 4 > 160 * 1024)
+        prune4_lds_bytes(kPruneWaves, w64, T) > 160 * 1024)
         return DICE_OK;
     // every table padded to the largest template count (704): each schedule reads its prefix.
     // Group counts A_g = |Lf_t ∩ g| clamped to bytes; the old and the v3 constants; the v3 CC
@@ -1229,7 +1324,7 @@ static int launch_prune3(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) 
 template <int J, int TJ>
 static int launch_prune4(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     constexpr int NW = kPruneWaves;
-    const size_t lds = prune3_lds_bytes(NW, c->w64, c->T) + (size_t)prune3_tj(c->T) * kWave * 4;   // + orig map
+    const size_t lds = prune4_lds_bytes(NW, c->w64, c->T);
     auto kern = dice_prune4<J, TJ, NW>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
@@ -1243,10 +1338,9 @@ static int launch_prune4(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) 
     pa.q8 = (const uint4*)c->d_p4q8;
     pa.tc = (const uint4*)c->d_p4tc;
     pa.ccm = (const uint32_t*)c->d_p4cc;
-    pa.qoff = (const uint32_t*)c->d_p4off;
+    pa.srec = (const uint32_t*)c->d_p4off;
     pa.qrec = (const uint4*)c->d_p4rec;
     pa.slot = (const uint4*)c->d_p4slot;
-    pa.orig = (const int32_t*)c->d_p4orig;
     for (int k = 0; k < 2; ++k) {
         pa.zkeep[k] = c->p4_zkeep[k];
         pa.zpos[k] = c->p4_zpos[k];
@@ -1279,7 +1373,7 @@ static int launch_prune4(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) 
 
 template <int J>
 static int launch_prune3_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    if (c->prune_sched != 6) {   // v4 unless v3 is asked for (A/B)
+    if (c->prune_sched != 6 && (!P4_ROW16 || (c->w64 & 1) == 0)) {   // v4 (16-byte row loads: even w64) unless v3
         switch (prune3_tj(c->T)) {
             case 2: return launch_prune4<J, 2>(c, b, thr, s);
             case 4: return launch_prune4<J, 4>(c, b, thr, s);
