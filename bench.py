@@ -291,6 +291,20 @@ def single_file_latency(run, n_calls=400):
         ts = np.array(ts) * 1e6
         out[name] = {'p50_us': float(np.percentile(ts, 50)), 'p99_us': float(np.percentile(ts, 99)),
                      'mean_us': float(ts.mean())}
+        # the same calls through the general path (scratch batch, pageable copies): the
+        # small-call path's gain (DICE_NO_SMALL_CALL is read per call)
+        os.environ['DICE_NO_SMALL_CALL'] = '1'
+        try:
+            for st in structs[:20]:
+                call(st)
+            tg = []
+            for st in structs[:200]:
+                t0 = time.perf_counter()
+                call(st)
+                tg.append(time.perf_counter() - t0)
+        finally:
+            os.environ.pop('DICE_NO_SMALL_CALL', None)
+        out[name]['general_path_p50_us'] = float(np.percentile(np.array(tg) * 1e6, 50))
     orc = oracle_for(run.corpus)
     m = min(4000, f.n)
     csr = bits_to_csr(f.bits[:m], run.corpus.n_vocab)
@@ -305,7 +319,8 @@ def single_file_latency(run, n_calls=400):
 def measure_extra(r, c, args, stream, sptr, cpu):
     steps = min(args.steps, 20)
     w, lm, ach = timed(r, steps, 2, stream, False)
-    tr, tr_src = traffic_for(c, r.n_per, r.T, '_post' if (c == 3 and r.match_kernel == 3) else '')
+    tr, tr_src = traffic_for(c if c != '5-T600' else '5_T600', r.n_per, r.T,
+                             '_post' if (c == 3 and r.match_kernel == 3) else '')
     rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'templates': r.T, 'vocab': r.V,
            'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': r.n_per * steps / w,
            'scores_per_s': r.n_per * steps / w * r.T, 'launch_ms': lm,
@@ -334,7 +349,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=100)
     ap.add_argument('--warmup', type=int, default=10)
-    ap.add_argument('--config', type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument('--config', type=lambda x: int(x) if x.isdigit() else x, default=2,
+                    choices=[2, 3, 4, 5, '5-T600'])
     ap.add_argument('--files-per-gpu', type=int, default=None)
     ap.add_argument('--threshold', type=float, default=98.0)
     ap.add_argument('--topk', type=int, default=3)
@@ -371,18 +387,20 @@ def main():
     cfg = args.config
     n_per = args.files_per_gpu or DEFAULT_FILES[cfg]
     run = Run(cfg, n_per, rank, world, dev, nthreads, args)
+    matrix_mode = run.cfg == 5            # configs 5 and 5-T600: full matrix + top-k
     stream = torch.cuda.Stream()          # a real (non-null) stream: kernels and HIP events share it
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, distributed)
     total_files = n_per * world
     value = total_files * args.steps / wall
-    traffic, traffic_src = traffic_for(cfg, n_per, run.T, '_post' if (cfg == 3 and run.match_kernel == 3) else '')
+    traffic, traffic_src = traffic_for(cfg if cfg != '5-T600' else '5_T600', n_per, run.T,
+                                       '_post' if (cfg == 3 and run.match_kernel == 3) else '')
     batch, files, corpus, synth = run.batch, run.files, run.corpus, run.synth
 
     # ---- results: gathers (outside the timed region) -------------------------
     extras = {}
-    if cfg != 5:
+    if not matrix_mode:
         t_g = time.perf_counter()
         best, ov, score = batch.download_match(sptr)
         host_gather_s = time.perf_counter() - t_g
@@ -407,7 +425,7 @@ def main():
             extras['gather_winner'] = 'host' if t[0] <= t[1] else 'rccl'
 
     # ---- separately reported rates (never `value`): PCIe-inclusive end-to-end, host prep ----
-    if rank == 0 and cfg != 5 and not args.probe:
+    if rank == 0 and not matrix_mode and not args.probe:
         torch.cuda.synchronize()
         t_e = time.perf_counter()
         batch.upload(files, sptr)
@@ -461,7 +479,7 @@ def main():
                                     f'native (csrc/normalize.cpp) {nthreads} threads on 16000 byte strings '
                                     f'(avg {sum(map(len, big)) / len(big) / 1024:.1f} KiB)')
 
-    if rank == 0 and cfg != 5 and not args.probe:
+    if rank == 0 and not matrix_mode and not args.probe:
         torch.cuda.synchronize()
         extras['single_file_us'] = single_file_latency(run)
 
@@ -495,7 +513,7 @@ def main():
                         'bitset_variant_files_per_s': sample / cpu_bits_s,
                         'nproc': cpu['nproc'], 'affinity_cpus': cpu['affinity_cpus'],
                         'cgroup_cpu_quota': cpu['cgroup_cpu_quota'], 'cpu_model': cpu['cpu_model']}
-        if cfg != 5:
+        if not matrix_mode:
             mism = int(np.sum(best[sl] != cb) + np.sum(ov[sl] != co) + np.sum(score[sl] != cs))
             parity = {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
         else:

@@ -188,6 +188,22 @@ int dice_batch_stream_probe(dice_batch *batch, void *stream);
 /* Bytes of the resident tile layout per file (the kernel's algorithmic input stream). */
 int64_t dice_batch_bytes_per_file(const dice_batch *batch);
 
+/* ---- Matchers::Exact on the device --------------------------------------------------
+ * Exact#match (exact.rb:6-12): the first template in key order (License.all, no CC filter)
+ * whose wordset (content_helper.rb:108-110: Lf plus the field words, :323-335) equals the
+ * file's. dice_exact_setup gives per template |wordset| ([T]), the field words that are
+ * vocabulary words as bits (field_bits [T][dice_words64(V)], NULL = none) and the field words
+ * outside the vocabulary as bits of the caller's numbering (field_need [T], NULL = none;
+ * licensee_host.h lh_template_field_masks). Per file, file_field_mask[i] (host, [n]; NULL =
+ * all zero) holds the same numbering's bits of the file's wordset (lh_prep_files).
+ * exact[i] = template index or -1. The kernel reads the batch's row-major bitsets (the
+ * stream probe overwrites them). dice_batch_exact is asynchronous on `stream`. */
+int dice_exact_setup(dice_ctx *ctx, const uint32_t *wordset_size, const uint64_t *field_bits,
+                     const uint64_t *field_need);
+int dice_batch_exact(dice_batch *batch, const uint64_t *file_field_mask, void *stream);
+int dice_batch_download_exact(dice_batch *batch, int32_t *exact, void *stream);
+int dice_exact(dice_ctx *ctx, const dice_files *files, const uint64_t *file_field_mask, int32_t *exact);
+
 /* Build step (no device needed): generate + compile the corpus-specialized sparse program
  * with hiprtc for gfx950 and store it in the code-object cache; writes the cache path. */
 int dice_precompile(const dice_templates *templates, char *path, int32_t path_cap);

@@ -37,6 +37,10 @@ void lh_destroy(lh_ctx *ctx);
 int lh_set_templates(lh_ctx *ctx, int32_t n_templates, const uint64_t *lf_bits,
                      const uint32_t *wordset_size, const int32_t *field_off,
                      const char *const *field_words);
+/* The template field words outside the vocabulary, numbered in first-appearance order: need[t]
+ * (if not NULL, [T]) gets bit k for each of template t's. Returns their count, -1 above 64.
+ * These masks and lh_prep_files' field_mask feed dice_exact_setup / dice_batch_exact. */
+int32_t lh_template_field_masks(lh_ctx *ctx, uint64_t *need);
 
 /* Unicode tables, so texts with non-ASCII letters stay native (without them the native
  * envelope is ASCII letters only). lower_*: every non-ASCII code point whose Python
@@ -50,11 +54,14 @@ int lh_set_unicode(lh_ctx *ctx, int32_t n_lower, const uint32_t *lower_from, con
 int64_t lh_normalize(lh_ctx *ctx, const char *data, int64_t len, const char *filename,
                      int32_t is_file, char *out, int64_t cap);
 
-/* Batched preparation of n LicenseFiles into dice_files arrays + matcher flags. */
+/* Batched preparation of n LicenseFiles into dice_files arrays + matcher flags.
+ * exact may be NULL (Exact then runs on the device: dice_batch_exact); field_mask, if not
+ * NULL, gets per file bit k = its wordset holds non-vocabulary field word k (-1 when the
+ * templates have more than 64 such words). */
 int lh_prep_files(lh_ctx *ctx, int64_t n, const char *const *data, const int64_t *lens,
                   const char *const *filenames, int32_t nthreads, uint64_t *bits, uint32_t *wf,
                   int32_t *length, uint8_t *cc, uint8_t *copyright, int32_t *exact,
-                  uint8_t *status);
+                  uint8_t *status, uint64_t *field_mask);
 
 /* Vocabulary packing (csrc/vocab_pack.cpp): local search over word swaps between bins of
  * bin_bits (32: sparse-program (template, dword) instruction pairs; 64: LDS-kernel

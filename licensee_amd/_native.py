@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = (
     'dice_last_error', 'dice_precompile', 'dice_program_source', 'dice_batch_stream_probe',
     'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids', 'dice_last_gather_peer',
     'dice_batch_deferred',
-    'dice_ctx_match_kernel',
+    'dice_ctx_match_kernel', 'dice_exact_setup', 'dice_batch_exact', 'dice_batch_download_exact', 'dice_exact',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -90,6 +90,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_deferred': (ctypes.c_int, [vp, ctypes.POINTER(i64), vp]),
         'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
         'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
+        'dice_exact_setup': (ctypes.c_int, [vp, vp, vp, vp]),
+        'dice_batch_exact': (ctypes.c_int, [vp, vp, vp]),
+        'dice_batch_download_exact': (ctypes.c_int, [vp, vp, vp]),
+        'dice_exact': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -225,6 +229,30 @@ class Scorer:
     def batch(self, capacity: int) -> 'DeviceBatch':
         return DeviceBatch(self, capacity)
 
+    def exact_setup(self, wordset_size, field_bits: Optional[np.ndarray] = None,
+                    field_need: Optional[np.ndarray] = None):
+        """Exact#match tables (exact.rb:6-12): |wordset| per template, the field words that are
+        vocabulary words as [T, words64(V)] bits, the others as [T] uint64 need masks."""
+        T = self.n_templates
+        ws = np.ascontiguousarray(wordset_size, dtype=np.uint32)
+        fb = None if field_bits is None else np.ascontiguousarray(field_bits, dtype=np.uint64)
+        fn = None if field_need is None else np.ascontiguousarray(field_need, dtype=np.uint64)
+        if ws.shape != (T,) or (fb is not None and fb.shape != (T, words64(self.n_vocab))) or \
+                (fn is not None and fn.shape != (T,)):
+            raise ValueError('exact tables: wordset_size [T], field_bits [T, words64(V)], field_need [T]')
+        _check(load_library().dice_exact_setup(self._ctx, _ptr(ws), _ptr(fb), _ptr(fn)))
+
+    def exact(self, files: FileBatch, field_mask: Optional[np.ndarray] = None) -> np.ndarray:
+        """Exact#match per file on the device: template index or -1."""
+        out = np.empty(files.n, np.int32)
+        if files.n:
+            fm = None if field_mask is None else np.ascontiguousarray(field_mask, dtype=np.uint64)
+            if fm is not None and fm.shape != (files.n,):
+                raise ValueError('field_mask must be [n]')
+            st = files._struct()
+            _check(load_library().dice_exact(self._ctx, ctypes.byref(st), _ptr(fm), _ptr(out)))
+        return out
+
 
 class DeviceBatch:
     """A device-resident batch (``dice_batch``): upload once, score many times."""
@@ -301,6 +329,19 @@ class DeviceBatch:
                                                          _ptr(tki) if k else None, _ptr(tks) if k else None,
                                                          stream or None))
         return ov, score, tki, tks
+
+    def exact(self, field_mask: Optional[np.ndarray] = None, stream: int = 0):
+        """Exact#match of the resident files (asynchronous; ``field_mask`` [n] uint64 or None)."""
+        fm = None if field_mask is None else np.ascontiguousarray(field_mask, dtype=np.uint64)
+        if fm is not None and fm.shape != (self.n,):
+            raise ValueError('field_mask must be [n]')
+        self._fm = fm   # the H2D copy may still read it after the call returns
+        _check(load_library().dice_batch_exact(self._b, _ptr(fm), stream or None))
+
+    def download_exact(self, stream: int = 0) -> np.ndarray:
+        out = np.empty(self.n, np.int32)
+        _check(load_library().dice_batch_download_exact(self._b, _ptr(out), stream or None))
+        return out
 
     def deferred(self, stream: int = 0) -> int:
         """Files the bound-pruned kernel handed to the postings kernels in the last match."""

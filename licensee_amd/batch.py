@@ -4,8 +4,12 @@ The reference evaluates ``[Copyright, Exact, Dice].map(new).find(&:match)`` per 
 (license_file.rb:67-69, project_file.rb:69-80) and falls back to ``License 'other'``
 (license_file.rb:92-98). Here the whole chain runs in bulk:
 
-  host (liblicensee_host.so, threads): decode, normalize, intern, Copyright, Exact
-  GPU  (liblicensee_dice.so):          Dice#match / #confidence for the files left
+  host (liblicensee_host.so, threads): decode, normalize, intern, Copyright, the per-file
+                                       mask of non-vocabulary field words
+  GPU  (liblicensee_dice.so):          Exact#match (dice_batch_exact: |W_F| == |W_t| and
+                                       W_t ⊆ W_F, exact.rb:6-12) and Dice#match / #confidence
+                                       on the same resident batch
+(``exact_on='host'`` keeps Exact in the host threads, the round-2 split.)
 
 Results equal the per-file Python chain (tests/test_gpu_golden.py::test_batch_chain).
 """
@@ -31,18 +35,36 @@ class BatchDetector:
     ``engine`` defaults to the process-wide :func:`dice.default_engine` (the vendored
     corpus); pass a :class:`dice.DiceEngine` to use another corpus or device."""
 
-    def __init__(self, engine=None, nthreads: int = 8):
+    def __init__(self, engine=None, nthreads: int = 8, exact_on: str = 'device'):
         from .dice import default_engine
         from .native_host import HostPrep
+        if exact_on not in ('device', 'host'):
+            raise ValueError("exact_on is 'device' or 'host'")
         self.engine = engine if engine is not None else default_engine()
         self.host = HostPrep(self.engine.corpus)
         self.nthreads = nthreads
+        self.exact_on = exact_on if self.host.field_need is not None else 'host'
+        if self.exact_on == 'device':
+            self.engine.scorer.exact_setup(*exact_tables(self.engine.corpus, self.host))
 
     def detect(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
                threshold=None) -> List[Detection]:
         thr = config.confidence_threshold() if threshold is None else threshold
-        fb, copyright, exact, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads)
-        best, _, score = self.engine.scorer.match(fb, float(thr))
+        if self.exact_on == 'device':
+            fb, copyright, fmask, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads,
+                                                           field_masks=True)
+            b = self.engine.scorer.batch(max(fb.n, 1))
+            try:
+                b.upload(fb)
+                b.exact(fmask)
+                b.match(float(thr))
+                exact = b.download_exact()
+                best, _, score = b.download_match()
+            finally:
+                b.close()
+        else:
+            fb, copyright, exact, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads)
+            best, _, score = self.engine.scorer.match(fb, float(thr))
         templates = self.engine.templates
         no_license, other = License.find('no-license'), License.find('other')
         out = []
@@ -56,3 +78,18 @@ class BatchDetector:
             else:
                 out.append(Detection(other, None, None))
         return out
+
+
+def exact_tables(corpus, host):
+    """dice_exact_setup's tables for a TemplateCorpus: |wordset| per template, its field words
+    that are vocabulary words as bitsets, the others as bits of ``host.nv_fields``
+    (content_helper.rb:323-335: wordset = wordset_fieldless + the field words)."""
+    import numpy as np
+    T = len(corpus.templates)
+    bits = np.zeros((T, corpus.w64), np.uint64)
+    for t, tpl in enumerate(corpus.templates):
+        for w in set(tpl.fields_normalized()):
+            i = corpus.index.get(w)
+            if i is not None:
+                bits[t, i >> 6] |= np.uint64(1 << (i & 63))
+    return host._ws, bits, host.field_need

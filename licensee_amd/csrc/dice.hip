@@ -272,6 +272,12 @@ int dalloc(T** p, size_t count) {
 
 static hipStream_t pick_stream(dice_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
 
+// A/B switch read per call (e.g. DICE_NO_SMALL_CALL=1: the small calls take the general path)
+static bool getenv_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && *v && *v != '0';
+}
+
 template <class E>
 static int transpose_to(dice_batch* b, const E* d_src, int64_t rows, int64_t cols, E* dst, hipStream_t s,
                         hipMemcpyKind kind) {
@@ -303,6 +309,9 @@ const char* dice_last_error(void) { return dice::last_error().c_str(); }
 static void ctx_free(dice_ctx* c) {
     if (!c) return;
     if (c->scratch) dice_batch_destroy(c->scratch);
+    if (c->small) dice_batch_destroy(c->small);
+    if (c->h_small_in) (void)hipHostFree(c->h_small_in);
+    if (c->h_small_out) (void)hipHostFree(c->h_small_out);
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
@@ -316,6 +325,7 @@ static void ctx_free(dice_ctx* c) {
         if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
     }
+    dice::exact_free(c);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -344,6 +354,7 @@ int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
     c->w64 = dice_words64(t->n_vocab);
     c->wq = (c->w64 + 1) / 2;
     c->tpad = ((c->T + kTT - 1) / kTT) * kTT;
+    c->h_lf.assign(t->lf_bits, t->lf_bits + (size_t)c->T * c->w64);   // Exact tables (dice_exact.hip)
     int rc;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         ctx_free(c);
@@ -420,9 +431,18 @@ int32_t dice_ctx_match_kernel(const dice_ctx* ctx) {
 void dice_batch_destroy(dice_batch* b) {
     if (!b) return;
     DeviceGuard g(b->ctx->device);
+    if (b->d_in) {   // carved small-call batch: the regions own these
+        b->d_wf = nullptr; b->d_len = nullptr; b->d_cc = nullptr; b->d_rows = nullptr;
+        (void)hipFree(b->d_in);
+    }
+    if (b->d_out) {
+        b->d_best = nullptr; b->d_ov = nullptr; b->d_score = nullptr;
+        b->d_mov = nullptr; b->d_mscore = nullptr; b->d_tki = nullptr; b->d_tks = nullptr;
+        (void)hipFree(b->d_out);
+    }
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
                     b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
-                    b->d_defer, b->d_ndefer};
+                    b->d_defer, b->d_ndefer, b->d_exact, b->d_fmask};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -745,11 +765,182 @@ int dice::scratch_for(dice_ctx* ctx, int64_t n, dice_batch** out) {
     return rc;
 }
 
+// ---- small host-buffer calls ---------------------------------------------------------------
+// licensee scores one file at a time (license_file.rb:92-98 -> dice.rb:34-41), so a drop-in
+// binding calls dice_match / dice_similarity_matrix with n = 1. For n <= kSmallFiles the call
+// packs its inputs into one page-locked region, copies it with one H2D into the small batch's
+// input region (scalars first, then the rows), runs the usual kernels, and brings every result
+// back with one D2H: two copies per call instead of seven, no pageable staging, no memsets.
+namespace {
+
+constexpr int64_t kSmallFiles = 64;
+constexpr size_t kAlign = 256;
+
+size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+struct SmallLayout {
+    size_t wf, len, cc, rows, in_bytes;                    // input region
+    size_t best, ov, score, mov, mscore, tki, tks, out_bytes;   // output region
+};
+
+SmallLayout small_layout(const dice_ctx* c) {
+    const size_t n = (size_t)kSmallFiles, T = (size_t)c->T, K = (size_t)DICE_TOPK_MAX;
+    SmallLayout L;
+    L.wf = 0;
+    L.len = L.wf + n * 4;
+    L.cc = L.len + n * 4;
+    L.rows = align_up(L.cc + n);
+    L.in_bytes = L.rows + n * (size_t)c->w64 * 8;
+    L.best = 0;
+    L.ov = L.best + n * 4;
+    L.score = L.ov + n * 4;
+    L.mov = align_up(L.score + n * 8);
+    L.mscore = align_up(L.mov + T * n * 4);
+    L.tki = align_up(L.mscore + T * n * 8);
+    L.tks = align_up(L.tki + K * n * 4);
+    L.out_bytes = L.tks + K * n * 8;
+    return L;
+}
+
+int small_batch(dice_ctx* c, dice_batch** out) {
+    if (c->small) {
+        *out = c->small;
+        return DICE_OK;
+    }
+    const SmallLayout L = small_layout(c);
+    dice_batch* b = nullptr;
+    int rc = dice_batch_create(c, kSmallFiles, &b);
+    if (rc) return rc;
+    void* old[] = {b->d_rows, b->d_wf, b->d_len, b->d_cc, b->d_best, b->d_ov, b->d_score};
+    for (void* p : old) (void)hipFree(p);
+    b->d_rows = nullptr; b->d_wf = nullptr; b->d_len = nullptr; b->d_cc = nullptr;
+    b->d_best = nullptr; b->d_ov = nullptr; b->d_score = nullptr;
+    if ((rc = dice::dalloc_bytes(&b->d_in, L.in_bytes)) || (rc = dice::dalloc_bytes(&b->d_out, L.out_bytes)) ||
+        (!c->h_small_in && hipHostMalloc(&c->h_small_in, L.in_bytes, hipHostMallocDefault) != hipSuccess) ||
+        (!c->h_small_out && hipHostMalloc(&c->h_small_out, L.out_bytes, hipHostMallocDefault) != hipSuccess)) {
+        dice_batch_destroy(b);
+        return rc ? rc : fail(DICE_E_NOMEM, "hipHostMalloc failed");
+    }
+    char* in = (char*)b->d_in;
+    char* o = (char*)b->d_out;
+    b->d_wf = (uint32_t*)(in + L.wf);
+    b->d_len = (int32_t*)(in + L.len);
+    b->d_cc = (uint8_t*)(in + L.cc);
+    b->d_rows = (uint64_t*)(in + L.rows);
+    b->d_best = (int32_t*)(o + L.best);
+    b->d_ov = (uint32_t*)(o + L.ov);
+    b->d_score = (double*)(o + L.score);
+    b->d_mov = (uint32_t*)(o + L.mov);
+    b->d_mscore = (double*)(o + L.mscore);
+    b->d_tki = (int32_t*)(o + L.tki);
+    b->d_tks = (double*)(o + L.tks);
+    b->mat_cap = kSmallFiles;
+    b->mat_k = DICE_TOPK_MAX;
+    c->small = b;
+    *out = b;
+    return DICE_OK;
+}
+
+// inputs -> the page-locked region -> one H2D; the tile repack for the tile-layout kernels
+int small_upload(dice_ctx* c, dice_batch* b, const dice_files* f, const SmallLayout& L) {
+    const int64_t n = f->n_files;
+    const int64_t npad = (n + kWave - 1) / kWave * kWave;
+    char* h = (char*)c->h_small_in;
+    std::memcpy(h + L.wf, f->wordset_size, (size_t)n * 4);
+    std::memset(h + L.wf + n * 4, 0, (size_t)(npad - n) * 4);
+    std::memcpy(h + L.len, f->length, (size_t)n * 4);
+    std::memset(h + L.len + n * 4, 0, (size_t)(npad - n) * 4);
+    std::memcpy(h + L.cc, f->cc_false_positive, (size_t)n);
+    std::memset(h + L.cc + n, 0, (size_t)(npad - n));
+    std::memcpy(h + L.rows, f->bits, (size_t)n * c->w64 * 8);
+    b->n = n;
+    HIP_TRY(hipMemcpyAsync(b->d_in, h, L.rows + (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, c->stream));
+    if (c->kind == 3) return DICE_OK;
+    const int64_t n_tiles = npad / kWave;
+    const int64_t total = n_tiles * c->wq * kWave;
+    hipLaunchKernelGGL(dice_pack_tiles, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       b->d_rows, n, c->w64, c->wq, c->kind == 1 ? (const int32_t*)c->d_qperm : nullptr, b->d_tiles,
+                       n_tiles);
+    HIP_TRY(hipGetLastError());
+    return DICE_OK;
+}
+
+int small_match(dice_ctx* c, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
+    DeviceGuard g(c->device);
+    dice_batch* b = nullptr;
+    int rc;
+    if ((rc = small_batch(c, &b))) return rc;
+    const SmallLayout L = small_layout(c);
+    if ((rc = small_upload(c, b, f, L)) || (rc = dice_batch_match(b, thr, nullptr))) return rc;
+    const size_t n = (size_t)f->n_files;
+    HIP_TRY(hipMemcpyAsync(c->h_small_out, b->d_out, L.score + n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const char* h = (const char*)c->h_small_out;
+    if (best) std::memcpy(best, h + L.best, n * 4);
+    if (ov) std::memcpy(ov, h + L.ov, n * 4);
+    if (score) std::memcpy(score, h + L.score, n * 8);
+    return DICE_OK;
+}
+
+int small_matrix(dice_ctx* c, const dice_files* f, uint32_t* ov, double* score, int32_t k, int32_t* tki,
+                 double* tks) {
+    DeviceGuard g(c->device);
+    dice_batch* b = nullptr;
+    int rc;
+    if ((rc = small_batch(c, &b))) return rc;
+    const SmallLayout L = small_layout(c);
+    // the matrix areas packed for this n ([T][n] or [n][T], [k][n] or [n][k]: n * T and n * k
+    // entries either way), so one D2H moves exactly the results
+    const size_t n = (size_t)f->n_files, T = (size_t)c->T, kk = (size_t)k;
+    const size_t o_mov = L.mov, o_msc = align_up(o_mov + n * T * 4), o_tki = align_up(o_msc + n * T * 8),
+                 o_tks = align_up(o_tki + n * kk * 4), o_end = o_tks + n * kk * 8;
+    char* d = (char*)b->d_out;
+    b->d_mov = (uint32_t*)(d + o_mov);
+    b->d_mscore = (double*)(d + o_msc);
+    b->d_tki = (int32_t*)(d + o_tki);
+    b->d_tks = (double*)(d + o_tks);
+    if ((rc = small_upload(c, b, f, L)) || (rc = dice_batch_matrix(b, k, nullptr))) return rc;
+    HIP_TRY(hipMemcpyAsync((char*)c->h_small_out + o_mov, d + o_mov, o_end - o_mov, hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const char* h = (const char*)c->h_small_out;
+    const uint32_t* hm = (const uint32_t*)(h + o_mov);
+    const double* hs = (const double*)(h + o_msc);
+    const int32_t* hi = (const int32_t*)(h + o_tki);
+    const double* hk = (const double*)(h + o_tks);
+    if (b->mat_rowmajor) {
+        if (ov) std::memcpy(ov, hm, n * T * 4);
+        if (score) std::memcpy(score, hs, n * T * 8);
+        if (k > 0) {
+            std::memcpy(tki, hi, n * kk * 4);
+            std::memcpy(tks, hk, n * kk * 8);
+        }
+        return DICE_OK;
+    }
+    for (size_t i = 0; i < n; ++i) {   // template-major [T][n] / [k][n]
+        for (size_t t = 0; t < T; ++t) {
+            if (ov) ov[i * T + t] = hm[t * n + i];
+            if (score) score[i * T + t] = hs[t * n + i];
+        }
+        for (size_t j = 0; j < kk; ++j) {
+            tki[i * kk + j] = hi[j * n + i];
+            tks[i * kk + j] = hk[j * n + i];
+        }
+    }
+    return DICE_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int dice_match(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
     if (!ctx || !f) return fail(DICE_E_ARG, "NULL ctx/files");
     if (f->n_files == 0) return DICE_OK;
+    if (f->n_files < 0) return fail(DICE_E_ARG, "n_files < 0");
+    if (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive)
+        return fail(DICE_E_ARG, "NULL file arrays");
+    if (f->n_files <= kSmallFiles && !getenv_flag("DICE_NO_SMALL_CALL")) return small_match(ctx, f, thr, best, ov, score);
     dice_batch* b = nullptr;
     int rc = dice::scratch_for(ctx, f->n_files, &b);
     if (rc) return rc;
@@ -764,6 +955,10 @@ int dice_similarity_matrix(dice_ctx* ctx, const dice_files* f, uint32_t* ov, dou
     if (k < 0 || k > DICE_TOPK_MAX) return fail(DICE_E_ARG, "k out of range");
     if (k > 0 && (!tki || !tks)) return fail(DICE_E_ARG, "top-k outputs required when k > 0");
     if (f->n_files == 0) return DICE_OK;
+    if (f->n_files < 0) return fail(DICE_E_ARG, "n_files < 0");
+    if (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive)
+        return fail(DICE_E_ARG, "NULL file arrays");
+    if (f->n_files <= kSmallFiles && !getenv_flag("DICE_NO_SMALL_CALL")) return small_matrix(ctx, f, ov, score, k, tki, tks);
     dice_batch* b = nullptr;
     int rc = dice::scratch_for(ctx, f->n_files, &b);
     if (rc) return rc;

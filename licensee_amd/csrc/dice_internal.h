@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "../../include/licensee_dice.h"
 #include "dice_program.h"
@@ -103,6 +104,15 @@ struct dice_ctx {
     void* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     size_t h_stage_bytes = 0;
+    // Exact matcher (dice_exact.hip): host copy of the Lf bitsets; templates sorted by |W_t|
+    // {|W_t|, t, record range}, need masks, records of W_t ∩ V
+    std::vector<uint64_t> h_lf;
+    // small host-buffer calls (n <= kSmallFiles, dice.hip): a batch whose inputs and results are
+    // each one device region, mirrored by page-locked host regions -- one H2D and one D2H per call
+    dice_batch* small = nullptr;
+    void *h_small_in = nullptr, *h_small_out = nullptr;
+    void *d_ex_tbl = nullptr, *d_ex_need = nullptr, *d_ex_rec = nullptr;
+    bool exact_ready = false;
 };
 
 namespace dice {
@@ -131,6 +141,8 @@ int download_match_to(dice_batch* b, int32_t* best, uint32_t* ov, double* score,
                       hipMemcpyKind kind);
 int download_matrix_to(dice_batch* b, uint32_t* ov, double* score, int32_t* tki, double* tks, hipStream_t s,
                        hipMemcpyKind kind);
+// the Exact tables (dice_exact.hip)
+void exact_free(dice_ctx* c);
 }  // namespace dice
 
 struct dice_batch {
@@ -163,4 +175,9 @@ struct dice_batch {
     // pruned match (dice_prune.hip): files deferred to the postings kernels
     int32_t* d_defer = nullptr;     // [capacity] file indices
     uint32_t* d_ndefer = nullptr;   // count
+    // Exact matcher (dice_batch_exact, lazily allocated): per-file result, field masks
+    int32_t* d_exact = nullptr;
+    uint64_t* d_fmask = nullptr;
+    // small-call batch: d_wf/d_len/d_cc/d_rows carved from d_in, results from d_out
+    void *d_in = nullptr, *d_out = nullptr;
 };

@@ -393,6 +393,10 @@ struct Ctx {
     std::vector<uint32_t> full_size;                // |wordset|
     std::vector<std::vector<std::string>> fields;   // field words in the wordset
     std::vector<std::vector<int32_t>> field_ids;    // their vocabulary ids, or -1
+    // field words outside the vocabulary, numbered in first-appearance order (bit k of a file's
+    // field mask / a template's need mask; at most 64 are numbered)
+    std::vector<std::string> nv_fields;
+    std::vector<uint64_t> field_need;               // [T]
     std::string err;
 
     const Regex& R(const char* name) const { return re.at(name); }
@@ -907,15 +911,30 @@ int lh_set_templates(lh_ctx* ctx, int32_t n_templates, const uint64_t* lf_bits, 
     c->full_size.assign(wordset_size, wordset_size + n_templates);
     c->fields.assign(n_templates, {});
     c->field_ids.assign(n_templates, {});
+    c->nv_fields.clear();
+    c->field_need.assign(n_templates, 0);
     for (int32_t t = 0; t < n_templates; ++t)
         for (int32_t k = field_off[t]; k < field_off[t + 1]; ++k) {
             c->fields[t].push_back(field_words[k]);
             // a field word can still be vocabulary (another template's word): then its presence is
             // the file's vocabulary bit, else the WordSet holds it
             const Str w = rx::from_utf8(field_words[k], strlen(field_words[k]));
-            c->field_ids[t].push_back(c->vocab.find(word_key(w.data(), w.size(), w.size()), w.data()));
+            const int32_t id = c->vocab.find(word_key(w.data(), w.size(), w.size()), w.data());
+            c->field_ids[t].push_back(id);
+            if (id >= 0) continue;
+            size_t j = 0;
+            while (j < c->nv_fields.size() && c->nv_fields[j] != field_words[k]) ++j;
+            if (j == c->nv_fields.size()) c->nv_fields.push_back(field_words[k]);
+            if (j < 64) c->field_need[(size_t)t] |= 1ULL << j;
         }
     return 0;
+}
+
+int32_t lh_template_field_masks(lh_ctx* ctx, uint64_t* need) {
+    const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+    if (!c || c->nv_fields.size() > 64) return -1;
+    if (need) std::copy(c->field_need.begin(), c->field_need.end(), need);
+    return (int32_t)c->nv_fields.size();
 }
 
 // Normalize one text. Returns UTF-8 byte count written to out (NUL-terminated when room),
@@ -951,11 +970,15 @@ int64_t lh_normalize(lh_ctx* ctx, const char* data, int64_t len, const char* fil
 // Batched LicenseFile preparation: decode, normalize, wordset scan, intern to the vocabulary
 // bitset, |W_F|, len_F, CC flag, Copyright and Exact matchers.
 //   status[i]: 0 ok; 1 the caller must use the Python path for file i (its outputs unset).
-//   exact[i]:  first template (key order) whose wordset equals the file's, or -1.
+//   exact[i]:  first template (key order) whose wordset equals the file's, or -1 (NULL: not
+//              computed -- the device decides Exact from field_mask, dice_batch_exact);
+//   field_mask[i] (NULL: not computed): bit k = the file's wordset holds the k-th field word
+//              outside the vocabulary (lh_template_field_masks).
 int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t* lens, const char* const* filenames,
                   int32_t nthreads, uint64_t* bits, uint32_t* wf, int32_t* length, uint8_t* cc, uint8_t* copyright,
-                  int32_t* exact, uint8_t* status) {
+                  int32_t* exact, uint8_t* status, uint64_t* field_mask) {
     const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+    if (field_mask && c->nv_fields.size() > 64) return -1;
     if (nthreads < 1) nthreads = 1;
     std::atomic<int64_t> next{0};
     auto work = [&]() {
@@ -988,6 +1011,13 @@ int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t
                 length[f] = (int32_t)o.normalized.size();
                 cc[f] = o.cc;
                 copyright[f] = o.copyright;
+                if (field_mask) {
+                    uint64_t m = 0;
+                    for (size_t k = 0; k < c->nv_fields.size(); ++k)
+                        if (words.contains(c->nv_fields[k])) m |= 1ULL << k;
+                    field_mask[f] = m;
+                }
+                if (!exact) continue;
                 int32_t ex = -1;
                 PASS("exact", for (int32_t t = 0; t < c->n_templates && ex < 0; ++t) {
                     if (c->full_size[t] != n_words) continue;

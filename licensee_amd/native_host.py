@@ -39,7 +39,9 @@ def _load():
         l.lh_normalize.restype = i64
         l.lh_normalize.argtypes = [vp, ctypes.c_char_p, i64, ctypes.c_char_p, i32, ctypes.c_char_p, i64]
         l.lh_prep_files.restype = ctypes.c_int
-        l.lh_prep_files.argtypes = [vp, i64, cpp, vp, cpp, i32, vp, vp, vp, vp, vp, vp, vp]
+        l.lh_prep_files.argtypes = [vp, i64, cpp, vp, cpp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+        l.lh_template_field_masks.restype = i32
+        l.lh_template_field_masks.argtypes = [vp, vp]
         l.lh_set_unicode.restype = ctypes.c_int
         l.lh_set_unicode.argtypes = [vp, i32, vp, vp, i32, vp, vp]
         _lib = l
@@ -138,6 +140,17 @@ class HostPrep:
             self._ws = ws
             self._lf = np.ascontiguousarray(corpus.lf_bits)
             lib.lh_set_templates(self._c, len(tpl), self._lf.ctypes.data, ws.ctypes.data, self._off.ctypes.data, fw)
+            # Exact on the device (dice_batch_exact): the field words outside the vocabulary,
+            # numbered in first-appearance order as the native side numbers them
+            vocab_set = set(corpus.vocab)
+            self.nv_fields = []
+            for f in fields:
+                if f not in vocab_set and f not in self.nv_fields:
+                    self.nv_fields.append(f)
+            need = np.zeros(len(tpl), np.uint64)
+            cnt = lib.lh_template_field_masks(self._c, need.ctypes.data)
+            self.field_need = need if cnt >= 0 else None
+            assert cnt == (len(self.nv_fields) if len(self.nv_fields) <= 64 else -1)
 
     def __del__(self):
         if getattr(self, '_c', None):
@@ -156,9 +169,11 @@ class HostPrep:
         return buf.raw[:n].decode('utf-8')
 
     def prep_files(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
-                   nthreads: int = 8) -> Tuple[FileBatch, np.ndarray, np.ndarray, np.ndarray]:
+                   nthreads: int = 8, field_masks: bool = False) -> Tuple[FileBatch, np.ndarray, np.ndarray, np.ndarray]:
         """Returns (FileBatch, copyright flags, exact template index or -1, fell_back mask).
-        Files the native path does not cover are prepared by the Python LicenseFile path."""
+        Files the native path does not cover are prepared by the Python LicenseFile path.
+        field_masks=True: Exact is left to the device (dice_batch_exact) and the third value is
+        instead each file's field mask (bit k = its wordset holds ``self.nv_fields[k]``)."""
         if self.corpus is None:
             raise ValueError('prep_files needs a TemplateCorpus')
         n = len(contents)
@@ -175,8 +190,15 @@ class HostPrep:
         cr = np.zeros(n, np.uint8)
         ex = np.full(n, -1, np.int32)
         st = np.zeros(n, np.uint8)
-        _load().lh_prep_files(self._c, n, data, lens.ctypes.data, fns, nthreads, bits.ctypes.data, wf.ctypes.data,
-                              ln.ctypes.data, cc.ctypes.data, cr.ctypes.data, ex.ctypes.data, st.ctypes.data)
+        fm = np.zeros(n, np.uint64) if field_masks else None
+        if field_masks and self.field_need is None:
+            raise ValueError('more than 64 template field words outside the vocabulary')
+        rc = _load().lh_prep_files(self._c, n, data, lens.ctypes.data, fns, nthreads, bits.ctypes.data,
+                                   wf.ctypes.data, ln.ctypes.data, cc.ctypes.data, cr.ctypes.data,
+                                   None if field_masks else ex.ctypes.data, st.ctypes.data,
+                                   fm.ctypes.data if field_masks else None)
+        if rc != 0:
+            raise RuntimeError('lh_prep_files failed')
         fell = st != 0
         if fell.any():
             from .matchers import Copyright, Exact
@@ -190,4 +212,9 @@ class HostPrep:
                 cr[i] = Copyright(lf).match() is not None
                 e = Exact(lf).match()
                 ex[i] = idx.get(e.key, -1) if e is not None else -1
+                if field_masks:
+                    ws = lf.wordset() or frozenset()
+                    fm[i] = sum(1 << k for k, w in enumerate(self.nv_fields) if w in ws)
+        if field_masks:
+            return FileBatch(bits, wf, ln, cc), cr.astype(bool), fm, fell
         return FileBatch(bits, wf, ln, cc), cr.astype(bool), ex, fell

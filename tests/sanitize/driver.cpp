@@ -103,8 +103,14 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> wf(n);
     std::vector<int32_t> length(n), exact(n);
     std::vector<uint8_t> cc(n), cr(n), st(n);
+    std::vector<uint64_t> fmask(n), need(T);
     if (lh_prep_files(ctx, n, data.data(), lens.data(), nullptr, 4, bits.data(), wf.data(), length.data(), cc.data(),
-                      cr.data(), exact.data(), st.data()))
+                      cr.data(), exact.data(), st.data(), nullptr))
+        return 6;
+    // the device-Exact variant: no host Exact, per-file field masks
+    if (lh_template_field_masks(ctx, need.data()) < 0 ||
+        lh_prep_files(ctx, n, data.data(), lens.data(), nullptr, 4, bits.data(), wf.data(), length.data(), cc.data(),
+                      cr.data(), nullptr, st.data(), fmask.data()))
         return 6;
     int64_t native = 0, total_len = 0;
     for (int64_t i = 0; i < n; ++i) {

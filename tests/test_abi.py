@@ -32,7 +32,7 @@ def test_host_library_exports_every_declared_symbol():
     lib = native_host._load()
     declared = declared_functions('licensee_host.h', 'lh_')
     assert declared == {'lh_create', 'lh_destroy', 'lh_set_templates', 'lh_set_unicode', 'lh_normalize', 'lh_prep_files',
-                        'lh_vocab_pack'}
+                        'lh_vocab_pack', 'lh_template_field_masks'}
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(os.listdir(os.path.join(ROOT, 'include'))) == {'licensee_dice.h', 'licensee_host.h'}

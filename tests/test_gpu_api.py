@@ -80,3 +80,45 @@ def test_device_batch_reuse_and_edges(corpus):
         b.matrix(17)                                     # k > DICE_TOPK_MAX
     b.close()
     sc.close()
+
+
+@pytest.mark.parametrize('large', [False, True])
+def test_small_calls_equal_general_path_and_oracle(corpus, large, monkeypatch):
+    """dice_match / dice_similarity_matrix with n <= 64 (the drop-in's one-file-per-call shape,
+    license_file.rb:92-98 -> dice.rb:34-41) take the one-H2D/one-D2H path: bit-identical to the
+    general path (DICE_NO_SMALL_CALL=1) and to the oracle, for the sparse program (T = 47) and
+    the T = 600 kernels (pruned match, postings matrix), across repeated calls and every k."""
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from licensee_amd.synth import SyntheticCorpus
+    from oracle.native import OracleScorer
+    c = corpus
+    if large:
+        from licensee_amd.synth_templates import synthetic_templates
+        c = TemplateCorpus(synthetic_templates(License.all(hidden=True, pseudo=False), 600, seed=20250202))
+    fb = SyntheticCorpus(c).generate(0, 200, seed=77, nthreads=4)
+    fb.cc_false_positive[::7] = 1
+    sc = _scorer(c)
+    orc = OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
+    from licensee_amd._native import FileBatch
+    for n in (1, 2, 63, 64):
+        for off in (0, 100):
+            sub = FileBatch(fb.bits[off:off + n], fb.wordset_size[off:off + n], fb.length[off:off + n],
+                            fb.cc_false_positive[off:off + n])
+            monkeypatch.delenv('DICE_NO_SMALL_CALL', raising=False)
+            fast_m = sc.match(sub, 98.0)
+            fast_x = [sc.matrix(sub, k) for k in (0, 3, 16)]
+            monkeypatch.setenv('DICE_NO_SMALL_CALL', '1')
+            gen_m = sc.match(sub, 98.0)
+            gen_x = [sc.matrix(sub, k) for k in (0, 3, 16)]
+            for a, b in zip(fast_m, gen_m):
+                assert np.array_equal(a, b), n
+            for fx, gx in zip(fast_x, gen_x):
+                for a, b in zip(fx, gx):
+                    assert np.array_equal(a, b), n
+            exp = orc.match(sub.bits, sub.wordset_size, sub.length, sub.cc_false_positive, 98.0, nthreads=2, mode=0)
+            for a, b in zip(fast_m, exp):
+                assert np.array_equal(a, b), n
+            mov, msc = orc.matrix(sub.bits, sub.wordset_size, sub.length, sub.cc_false_positive, nthreads=2)
+            assert np.array_equal(fast_x[1][0], mov) and np.array_equal(fast_x[1][1], msc)
+    sc.close()

@@ -165,6 +165,30 @@ def test_batch_prep_matches_python(hp):
         assert ex[i] == (keys.index(e.key) if e is not None else -1), i
 
 
+def test_field_masks_match_python(hp):
+    """lh_prep_files' per-file field masks (device Exact, dice_batch_exact): bit k = the file's
+    wordset holds the k-th template field word outside the vocabulary; the template need masks
+    (lh_template_field_masks) hold the same words of each template's fields_normalized."""
+    corpus = hp.corpus
+    assert hp.nv_fields, 'the vendored templates have field words outside the vocabulary (fullname)'
+    for t, tpl in enumerate(corpus.templates):
+        fs = set(tpl.fields_normalized())
+        assert int(hp.field_need[t]) == sum(1 << k for k, w in enumerate(hp.nv_fields) if w in fs), tpl.key
+    ncsa = License.find('ncsa').content_normalized()
+    assert '[fullname]' in ncsa
+    texts = [ncsa, ncsa.replace('[fullname]', 'zzzq'), ncsa.replace('[fullname]', 'fullname'), 'fullname only',
+             'ΣΟΦΙΑ fullname', '', 'year project fullname']
+    texts += [License.find(k).content_normalized() for k in ('bsd-3-clause', 'gpl-3.0', 'isc')]
+    fb, cr, fm, fell = hp.prep_files(texts, ['LICENSE'] * len(texts), nthreads=3, field_masks=True)
+    assert fell.sum() == 1
+    fb2, cr2, _, _ = hp.prep_files(texts, ['LICENSE'] * len(texts), nthreads=3)
+    assert np.array_equal(fb.bits, fb2.bits) and np.array_equal(fb.wordset_size, fb2.wordset_size)
+    assert np.array_equal(cr, cr2)
+    for i, t in enumerate(texts):
+        ws = LicenseFile(t, 'LICENSE').wordset() or frozenset()
+        assert int(fm[i]) == sum(1 << k for k, w in enumerate(hp.nv_fields) if w in ws), i
+
+
 def test_wordset_token_fuzz(hp):
     """The wordset scan (content_helper.rb:109, (?:[\\w/-](?:'s|(?<=s)')?)+) on texts dense in its
     corner cases: apostrophes after 's' and before 's' (including "it's'" where the 's' taken by

@@ -18,13 +18,13 @@ def load_counters(path, kernel):
 
 
 def main():
-    src, tag, config, files, templates = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    src, tag, config, files, templates = sys.argv[1], sys.argv[2], sys.argv[3].replace('-', '_'), int(sys.argv[4]), int(sys.argv[5])
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_stats.csv'))))
     # the product kernels of the timed region (copies/packing outside it are listed, not chosen):
     # the sparse program / dense / LDS kernels run one launch per step, the postings path two
     # (dice_post_dense + dice_post_narrow_*): a step's time and traffic sum over them
-    prefixes = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune_', 'dice_defer_')
+    prefixes = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune', 'dice_defer_')
     def base(r):
         return r['Name'].split('(')[0].replace('void ', '').replace('dice::', '')
     product = [r for r in stats if base(r).startswith(prefixes)]
