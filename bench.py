@@ -80,11 +80,17 @@ def cpu_info():
             'nproc': os.cpu_count(), 'cpu_model': model}
 
 
-def build_workload(config: int):
+def build_workload(config: int, corpus: str = 'synthetic'):
+    """The template corpus of a config. Config 3's ~600 templates: 'synthetic' = the 47 vendored
+    templates + synthetic ones; 'spdx' = 94 real texts (the 47 choosealicense.com templates and
+    the 47 SPDX license-list-XML texts, licensee_amd/spdx.py) + synthetic ones."""
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.license import License
     templates = License.all(hidden=True, pseudo=False)
-    if config == 3:
+    if config == 3 and corpus == 'spdx':
+        from licensee_amd.spdx import corpus_with_spdx
+        templates = corpus_with_spdx(templates, total=600)
+    elif config == 3:
         from licensee_amd.synth_templates import synthetic_templates
         templates = synthetic_templates(templates, 600, seed=20250202)
     return TemplateCorpus(templates)
@@ -120,7 +126,7 @@ class Run:
             corpus_cfg = cfg
         self.cfg, self.n_per, self.args = cfg, n_per, args
         t0 = time.time()
-        self.corpus = build_workload(corpus_cfg)
+        self.corpus = build_workload(corpus_cfg, getattr(args, 'corpus', 'synthetic'))
         self.synth = SyntheticCorpus(self.corpus, profile=1 if cfg == 4 else 0)
         first, count = shard_range(rank, world, n_per)
         self.files = self.synth.generate(first, count, seed=20250202, nthreads=nthreads)
@@ -359,6 +365,12 @@ def main():
     ap.add_argument('--extra-configs', default='3,4,5,5-T600',
                     help="configs also measured at N=1 (reported under extras.configs); '' for none")
     ap.add_argument('--probe', action='store_true', help='diagnostic: stream-read the tiles only (read ceiling)')
+    ap.add_argument('--corpus', default='synthetic', choices=['synthetic', 'spdx'],
+                    help="config 3's templates: synthetic, or the 94 real texts (47 choosealicense.com + 47 SPDX "
+                         "license-list-XML) + synthetic ones")
+    ap.add_argument('--no-extras', action='store_true',
+                    help='skip the separately reported host-side rates (PCIe end-to-end, host prep, single-file '
+                         'calls): profiling runs then trace only the timed workload')
     args = ap.parse_args()
 
     # stdout carries exactly one JSON line: anything native libraries print there (RCCL's
@@ -388,6 +400,7 @@ def main():
     n_per = args.files_per_gpu or DEFAULT_FILES[cfg]
     run = Run(cfg, n_per, rank, world, dev, nthreads, args)
     matrix_mode = run.cfg == 5            # configs 5 and 5-T600: full matrix + top-k
+    run_T_cfg3 = cfg in (3, '5-T600')     # config 3's template corpus
     stream = torch.cuda.Stream()          # a real (non-null) stream: kernels and HIP events share it
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
@@ -425,7 +438,7 @@ def main():
             extras['gather_winner'] = 'host' if t[0] <= t[1] else 'rccl'
 
     # ---- separately reported rates (never `value`): PCIe-inclusive end-to-end, host prep ----
-    if rank == 0 and not matrix_mode and not args.probe:
+    if rank == 0 and not matrix_mode and not args.probe and not args.no_extras:
         torch.cuda.synchronize()
         t_e = time.perf_counter()
         batch.upload(files, sptr)
@@ -479,7 +492,7 @@ def main():
                                     f'native (csrc/normalize.cpp) {nthreads} threads on 16000 byte strings '
                                     f'(avg {sum(map(len, big)) / len(big) / 1024:.1f} KiB)')
 
-    if rank == 0 and not matrix_mode and not args.probe:
+    if rank == 0 and not matrix_mode and not args.probe and not args.no_extras:
         torch.cuda.synchronize()
         extras['single_file_us'] = single_file_latency(run)
 
@@ -548,7 +561,9 @@ def main():
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
             'data': 'synthetic (normalized-space perturbations of the vendored templates, filler words from '
                     'the reference spec/fixtures/ipsum.txt, seed 20250202)',
-            'config': {'workload': WORKLOADS[cfg], 'files_per_gpu': n_per, 'global_files': total_files,
+            'config': {'workload': WORKLOADS[cfg] + (' (templates: 94 real texts incl. SPDX + synthetic)'
+                                                     if args.corpus == 'spdx' and run_T_cfg3 else ''),
+                       'files_per_gpu': n_per, 'global_files': total_files,
                        'templates': head['templates'], 'vocab': head['vocab'], 'kernel': head['kernel'],
                        'program_entries': head['program_entries'], 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',

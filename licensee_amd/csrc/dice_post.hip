@@ -286,45 +286,51 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
 
 // Phase 3 for one file: lanes = templates (t = lane + 64 j), overlap from the counter row
 // (the next file's copy-in overwrites every entry), the shared denominator and order; match
-// mode reduces over the wave, matrix mode writes the row and the top-k.
-template <bool kMatrix, int KM, int TJ>
-__device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
-                                           int32_t lf, bool cc, bool corpus_fast, double thr, int32_t* __restrict__ best_out,
-                                           uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
-                                           uint32_t* __restrict__ mov, double* __restrict__ msc, int32_t* __restrict__ tki,
-                                           double* __restrict__ tks, int lane) {
+// mode reduces over the wave, matrix mode writes the row and the top-k. Every lane keeps only
+// its best template; the top-k is k rounds of a wave argmax in which the winning lane marks its
+// template taken and rescans its other templates (from the LDS row) for its next best -- the
+// order of k argmaxes with removal, i.e. Dice#matches_by_similarity's (dice.rb:34-41), with one
+// candidate per lane instead of k sorted slots (the matrix kernel keeps the match kernel's
+// register budget and occupancy).
+template <bool FAST>
+__device__ __forceinline__ void lane_best(const uint32_t* crow32, const uint2* tcs, int32_t t, uint32_t wf, int32_t lf,
+                                          bool cc, int32_t& bi, uint32_t& bo, int32_t& bd, uint32_t& ov,
+                                          int32_t& den) {
+    ov = crow32[t];
+    const uint2 pc = tcs[t];   // {len | cc << 31, base | slack << 16}
+    const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
+                             (int32_t)(pc.x >> 31));
+    den = dice_den(c, wf, lf);
+    if (!(c.w && cc) && (bi < 0 || ge<FAST>(ov, den, bo, bd))) {
+        bi = t;
+        bo = ov;
+        bd = den;
+    }
+}
+
+template <bool kMatrix, int TJ, bool FAST>
+__device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
+                                             int32_t lf, bool cc, double thr, int32_t* __restrict__ best_out,
+                                             uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
+                                             uint32_t* __restrict__ mov, double* __restrict__ msc,
+                                             int32_t* __restrict__ tki, double* __restrict__ tks, int lane) {
     int32_t bi = -1, bd = 1;
     uint32_t bo = 0;
-    TopK<KM> top;
-    if (kMatrix) top.init();
-    // file inside the fast envelope (wave-uniform): 24-bit exact compares
-    const bool fast = corpus_fast && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
         const int32_t t = lane + j * kWave;
         if (t < T) {
-            const uint32_t ov = crow32[t];
-            const uint2 pc = tcs[t];   // {len | cc << 31, base | slack << 16}
-            const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
-                                     (int32_t)(pc.x >> 31));
-            const int32_t den = dice_den(c, wf, lf);
+            uint32_t ov;
+            int32_t den;
+            lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             if (kMatrix) {
-                mov[file * T + t] = ov;
-                msc[file * T + t] = dice_score(ov, den);
-            }
-            if (!(c.w && cc)) {
-                if (kMatrix) top.offer(t, ov, den);
-                else if (bi < 0 || (fast ? ge<true>(ov, den, bo, bd) : ge<false>(ov, den, bo, bd))) {
-                    bi = t;
-                    bo = ov;
-                    bd = den;
-                }
+                __builtin_nontemporal_store(ov, &mov[file * T + t]);
+                __builtin_nontemporal_store(dice_score(ov, den), &msc[file * T + t]);
             }
         }
     }
     if (!kMatrix) {
-        if (fast) wave_best<true>(bi, bo, bd);
-        else wave_best<false>(bi, bo, bd);
+        wave_best<FAST>(bi, bo, bd);
         if (lane == 0) {
             const double s = bi >= 0 ? dice_score(bo, bd) : 0.0;
             best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
@@ -332,24 +338,53 @@ __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, i
             score_out[file] = s;
         }
     } else if (tki) {
-        // k rounds of a wave argmax over the lanes' sorted heads
-        int h = 0;
+        uint32_t taken = 0;   // bit j: template lane + 64 j already ranked
         for (int r = 0; r < k; ++r) {
-            int32_t ci = -1, cd = 1;
-            uint32_t co = 0;
-#pragma unroll
-            for (int j = 0; j < KM; ++j)
-                if (j == h) { ci = top.idx[j]; co = top.ov[j]; cd = top.den[j]; }
-            int32_t wi = ci, wd = cd;
-            uint32_t wo = co;
-            wave_best(wi, wo, wd);
-            if (wi >= 0 && wi == ci) ++h;          // the winning lane advances
+            int32_t wi = bi, wd = bd;
+            uint32_t wo = bo;
+            wave_best<FAST>(wi, wo, wd);
             if (lane == 0) {
                 tki[file * k + r] = wi;
                 tks[file * k + r] = wi >= 0 ? dice_score(wo, wd) : -1.0;
             }
+            if (wi < 0) {   // every potential match ranked: pad the rest (wave-uniform)
+                for (int q = r + 1 + lane; q < k; q += kWave) {
+                    tki[file * k + q] = -1;
+                    tks[file * k + q] = -1.0;
+                }
+                break;
+            }
+            if (r + 1 < k && wi == bi) {   // the owner lane: next best among its untaken templates
+                taken |= 1u << (wi >> 6);
+                bi = -1;
+                bo = 0;
+                bd = 1;
+                for (int j = 0; j < TJ; ++j) {
+                    const int32_t t = lane + j * kWave;
+                    if (t < T && !((taken >> j) & 1u)) {
+                        uint32_t ov;
+                        int32_t den;
+                        lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
+                    }
+                }
+            }
         }
     }
+}
+
+template <bool kMatrix, int KM, int TJ>
+__device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
+                                           int32_t lf, bool cc, bool corpus_fast, double thr, int32_t* __restrict__ best_out,
+                                           uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
+                                           uint32_t* __restrict__ mov, double* __restrict__ msc, int32_t* __restrict__ tki,
+                                           double* __restrict__ tks, int lane) {
+    // file inside the fast envelope (wave-uniform): 24-bit exact compares
+    if (corpus_fast && wf < (1u << 20) && lf >= 0 && lf < (1 << 21))
+        score_file_t<kMatrix, TJ, true>(crow32, tcs, T, file, wf, lf, cc, thr, best_out, ov_out, score_out, k, mov,
+                                        msc, tki, tks, lane);
+    else
+        score_file_t<kMatrix, TJ, false>(crow32, tcs, T, file, wf, lf, cc, thr, best_out, ov_out, score_out, k, mov,
+                                         msc, tki, tks, lane);
 }
 
 // A file's loads that do not depend on its walk -- dense partials, scalars, first word chunks --
@@ -478,8 +513,13 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
                                score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn);
 }
 
+// POST_MATRIX_OCC (A/B): waves per SIMD the matrix kernel is compiled for (8: two workgroups
+// per CU as in match mode, at 64 VGPRs)
+#ifndef POST_MATRIX_OCC
+#define POST_MATRIX_OCC 8
+#endif
 template <int KM, int TPMAX>
-__global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
+__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(POST_MATRIX_OCC, POST_MATRIX_OCC))) void dice_post_narrow_matrix(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
@@ -488,7 +528,7 @@ __global__ __launch_bounds__(kPostWaves * kWave) void dice_post_narrow_matrix(
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
     post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, false, idx, pn);
+                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn);
 }
 
 // ---- host side ---------------------------------------------------------------------------
@@ -677,8 +717,8 @@ int post_launch_match_indexed(dice_ctx* c, dice_batch* b, double thr, const int3
 }
 
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s) {
-    // a lane holds at most kPostMaxTpad / 64 templates: that many top-k slots serve any k <= 16
-    return k <= 4 ? launch<true, 4>(c, b, 0.0, k, s) : launch<true, kPostMaxTpad / kWave>(c, b, 0.0, k, s);
+    // any k <= 16: one candidate per lane, k wave argmax rounds (score_file_t)
+    return launch<true, 1>(c, b, 0.0, k, s);
 }
 
 }  // namespace dice

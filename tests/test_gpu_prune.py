@@ -193,3 +193,21 @@ def test_t700(monkeypatch):
     fb = SyntheticCorpus(c).generate(0, 5000, seed=701, nthreads=16)
     _check(c, fb, monkeypatch)
     _check(c, _random_files(c, 500, seed=702, density=0.03), monkeypatch, thresholds=(0.0,))
+
+
+def test_batch_match_is_asynchronous_and_capturable():
+    """dice_batch_match's contract (licensee_dice.h): no host synchronization and no D2H inside,
+    also when the pruned kernel defers files to the postings kernels (their count stays on the
+    device). tests/async_capture_worker.py: (1) enqueued behind a ~0.2 s device sleep on the same
+    stream, the call returns long before the sleep ends; (2) captured into a hipGraph
+    (torch.cuda.CUDAGraph) and replayed twice, the results equal the oracle's -- with deferred
+    files (DICE_PRUNE_MAX_EVALS=1). Run in a child process so torch's HIP runtime initializes
+    before the library's (the order bench.py uses)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, 'tests', 'async_capture_worker.py')], cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert 'async ok' in r.stdout and 'capture ok' in r.stdout, r.stdout

@@ -16,7 +16,7 @@ timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/$
 cat gpurun_out/${TAG}_bench.json
 OUT=gpurun_out/prof_${TAG}_same
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python bench.py --extra-configs= --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || exit 12
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python bench.py --extra-configs= --no-cpu-baseline --no-extras > $OUT/bench.json 2> $OUT/bench.err || exit 12
 echo same_session_trace_done
 for c in $CONFIGS; do
   bash tools/profile_round.sh ${TAG}_config$c --config $c || exit $((20 + c))

@@ -7,7 +7,7 @@ TAG=$1; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --extra-configs= $*"
+B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras --extra-configs= $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B > $OUT/trace.json 2>$OUT/trace.err || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B > $OUT/fetch.json 2>$OUT/fetch.err || exit 2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $B > $OUT/write.json 2>$OUT/write.err || exit 3
