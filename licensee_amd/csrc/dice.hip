@@ -603,6 +603,8 @@ int dice_batch_match(dice_batch* b, double thr, void* stream) {
 
 static int ensure_matrix(dice_batch* b, int32_t k) {
     dice_ctx* c = b->ctx;
+    // row stride: kind 3 writes [n][post_ld] rows of whole 128-byte lines, the others [T][n]
+    b->mat_ld = c->kind == 3 ? c->post_ld : c->T;
     if (b->mat_cap >= b->capacity && b->mat_k >= k && b->d_mov) return DICE_OK;
     void* ptrs[] = {b->d_mov, b->d_mscore, b->d_tki, b->d_tks};
     for (void* p : ptrs)
@@ -610,8 +612,8 @@ static int ensure_matrix(dice_batch* b, int32_t k) {
     b->d_mov = nullptr; b->d_mscore = nullptr; b->d_tki = nullptr; b->d_tks = nullptr;
     int rc;
     const int32_t kk = std::max<int32_t>(k, 1);
-    if ((rc = dalloc(&b->d_mov, (size_t)b->capacity * c->T)) ||
-        (rc = dalloc(&b->d_mscore, (size_t)b->capacity * c->T)) ||
+    if ((rc = dalloc(&b->d_mov, (size_t)b->capacity * b->mat_ld)) ||
+        (rc = dalloc(&b->d_mscore, (size_t)b->capacity * b->mat_ld)) ||
         (rc = dalloc(&b->d_tki, (size_t)b->capacity * kk)) || (rc = dalloc(&b->d_tks, (size_t)b->capacity * kk)))
         return rc;
     b->mat_cap = b->capacity;
@@ -675,9 +677,10 @@ int download_matrix_to(dice_batch* b, uint32_t* ov, double* score, int32_t* tki,
     if (n && !b->d_mov) return fail(DICE_E_STATE, "dice_batch_matrix was not run");
     if (!n) return DICE_OK;
     int rc;
-    if (b->mat_rowmajor) {   // already [n][T] / [n][k]
-        if (ov) HIP_TRY(hipMemcpyAsync(ov, b->d_mov, (size_t)n * c->T * 4, kind, s));
-        if (score) HIP_TRY(hipMemcpyAsync(score, b->d_mscore, (size_t)n * c->T * 8, kind, s));
+    if (b->mat_rowmajor) {   // already [n][ld] / [n][k]: rows of T entries at stride ld
+        const size_t T = (size_t)c->T, ld = (size_t)b->mat_ld;
+        if (ov) HIP_TRY(hipMemcpy2DAsync(ov, T * 4, b->d_mov, ld * 4, T * 4, (size_t)n, kind, s));
+        if (score) HIP_TRY(hipMemcpy2DAsync(score, T * 8, b->d_mscore, ld * 8, T * 8, (size_t)n, kind, s));
         if (tki && b->k_used) HIP_TRY(hipMemcpyAsync(tki, b->d_tki, (size_t)n * b->k_used * 4, kind, s));
         if (tks && b->k_used) HIP_TRY(hipMemcpyAsync(tks, b->d_tks, (size_t)n * b->k_used * 8, kind, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -784,7 +787,7 @@ struct SmallLayout {
 };
 
 SmallLayout small_layout(const dice_ctx* c) {
-    const size_t n = (size_t)kSmallFiles, T = (size_t)c->T, K = (size_t)DICE_TOPK_MAX;
+    const size_t n = (size_t)kSmallFiles, T = (size_t)std::max(c->T, c->post_ld), K = (size_t)DICE_TOPK_MAX;
     SmallLayout L;
     L.wf = 0;
     L.len = L.wf + n * 4;
@@ -892,7 +895,8 @@ int small_matrix(dice_ctx* c, const dice_files* f, uint32_t* ov, double* score, 
     // the matrix areas packed for this n ([T][n] or [n][T], [k][n] or [n][k]: n * T and n * k
     // entries either way), so one D2H moves exactly the results
     const size_t n = (size_t)f->n_files, T = (size_t)c->T, kk = (size_t)k;
-    const size_t o_mov = L.mov, o_msc = align_up(o_mov + n * T * 4), o_tki = align_up(o_msc + n * T * 8),
+    const size_t ld = c->kind == 3 ? (size_t)c->post_ld : T;   // row-major rows at stride ld (kind 3)
+    const size_t o_mov = L.mov, o_msc = align_up(o_mov + n * ld * 4), o_tki = align_up(o_msc + n * ld * 8),
                  o_tks = align_up(o_tki + n * kk * 4), o_end = o_tks + n * kk * 8;
     char* d = (char*)b->d_out;
     b->d_mov = (uint32_t*)(d + o_mov);
@@ -909,8 +913,10 @@ int small_matrix(dice_ctx* c, const dice_files* f, uint32_t* ov, double* score, 
     const int32_t* hi = (const int32_t*)(h + o_tki);
     const double* hk = (const double*)(h + o_tks);
     if (b->mat_rowmajor) {
-        if (ov) std::memcpy(ov, hm, n * T * 4);
-        if (score) std::memcpy(score, hs, n * T * 8);
+        for (size_t i = 0; i < n; ++i) {
+            if (ov) std::memcpy(ov + i * T, hm + i * ld, T * 4);
+            if (score) std::memcpy(score + i * T, hs + i * ld, T * 8);
+        }
         if (k > 0) {
             std::memcpy(tki, hi, n * kk * 4);
             std::memcpy(tks, hk, n * kk * 8);

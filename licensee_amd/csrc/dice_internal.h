@@ -80,7 +80,7 @@ struct dice_ctx {
     void* d_povf = nullptr;    // flat u16 template ids of the long words
     void* d_pdm = nullptr;     // [T][16] u64 dense-prefix masks
     void* d_ptc = nullptr;     // [T] int4 template constants
-    int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0;
+    int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0, post_ld = 0;
     bool post_fast = false;
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): per-template group counts, records
@@ -96,7 +96,7 @@ struct dice_ctx {
     void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
          *d_p4slot = nullptr, *d_p4orig = nullptr;
     int32_t p4_zkeep[2] = {-1, -1}, p4_zpos[2] = {0, 0};
-    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12;
+    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12, prune_gq = 2;
     int64_t prune_records = 0;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
     // two page-locked staging buffers for shard uploads from pageable caller memory
@@ -160,7 +160,8 @@ struct dice_batch {
     int64_t mat_cap = 0;
     int32_t mat_k = 0;
     int32_t k_used = 0;
-    bool mat_rowmajor = false;      // kind 3 writes [n][T] / [n][k] directly (no transpose)
+    bool mat_rowmajor = false;      // kind 3 writes [n][ld] / [n][k] directly (no transpose)
+    int32_t mat_ld = 0;             // row stride (templates) of the row-major matrix
     uint32_t* d_mov = nullptr;      // template-major [T][capacity] (coalesced stores)
     double* d_mscore = nullptr;     // template-major [T][capacity]
     int32_t* d_tki = nullptr;

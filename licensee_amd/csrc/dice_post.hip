@@ -309,7 +309,7 @@ __device__ __forceinline__ void lane_best(const uint32_t* crow32, const uint2* t
 }
 
 template <bool kMatrix, int TJ, bool FAST>
-__device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
+__device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs, int32_t T, int32_t ld, int64_t file, uint32_t wf,
                                              int32_t lf, bool cc, double thr, int32_t* __restrict__ best_out,
                                              uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
                                              uint32_t* __restrict__ mov, double* __restrict__ msc,
@@ -324,8 +324,8 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             int32_t den;
             lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             if (kMatrix) {
-                __builtin_nontemporal_store(ov, &mov[file * T + t]);
-                __builtin_nontemporal_store(dice_score(ov, den), &msc[file * T + t]);
+                __builtin_nontemporal_store(ov, &mov[file * ld + t]);
+                __builtin_nontemporal_store(dice_score(ov, den), &msc[file * ld + t]);
             }
         }
     }
@@ -373,17 +373,17 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
 }
 
 template <bool kMatrix, int KM, int TJ>
-__device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, int32_t T, int64_t file, uint32_t wf,
+__device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, int32_t T, int32_t ld, int64_t file, uint32_t wf,
                                            int32_t lf, bool cc, bool corpus_fast, double thr, int32_t* __restrict__ best_out,
                                            uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
                                            uint32_t* __restrict__ mov, double* __restrict__ msc, int32_t* __restrict__ tki,
                                            double* __restrict__ tks, int lane) {
     // file inside the fast envelope (wave-uniform): 24-bit exact compares
     if (corpus_fast && wf < (1u << 20) && lf >= 0 && lf < (1 << 21))
-        score_file_t<kMatrix, TJ, true>(crow32, tcs, T, file, wf, lf, cc, thr, best_out, ov_out, score_out, k, mov,
+        score_file_t<kMatrix, TJ, true>(crow32, tcs, T, ld, file, wf, lf, cc, thr, best_out, ov_out, score_out, k, mov,
                                         msc, tki, tks, lane);
     else
-        score_file_t<kMatrix, TJ, false>(crow32, tcs, T, file, wf, lf, cc, thr, best_out, ov_out, score_out, k, mov,
+        score_file_t<kMatrix, TJ, false>(crow32, tcs, T, ld, file, wf, lf, cc, thr, best_out, ov_out, score_out, k, mov,
                                          msc, tki, tks, lane);
 }
 
@@ -430,7 +430,7 @@ __device__ __forceinline__ void post_narrow_body(
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
-    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
+    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
     // diag (DICE_POST_DIAG, diagnostics only -- results are wrong): 2 skips the postings walk,
     // 4 skips the narrow-word extraction, 8 skips scoring
     constexpr int kTJ = (TPMAX + kWave - 1) / kWave;           // templates per lane
@@ -492,7 +492,7 @@ __device__ __forceinline__ void post_narrow_body(
         }
 
         if (diag & 8) continue;
-        score_file<kMatrix, KM, kTJ>(crow32, tcs, T, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
+        score_file<kMatrix, KM, kTJ>(crow32, tcs, T, ld, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
                                             k, mov, msc, tki, tks, lane);
     }
     }
@@ -508,9 +508,9 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
-    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
+    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
     post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn);
+                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn, ld);
 }
 
 // POST_MATRIX_OCC (A/B): waves per SIMD the matrix kernel is compiled for (8: two workgroups
@@ -526,9 +526,9 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
-    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn) {
+    const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
     post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn);
+                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn, ld);
 }
 
 // ---- host side ---------------------------------------------------------------------------
@@ -645,6 +645,9 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
             c->post_fast = false;
     }
     c->post_tp = (T + 7) / 8 * 8;
+    // matrix rows of whole 128-byte lines ([n][ld] u32 and f64): no row shares a line with the next
+    // file's (another wave's) -- partial-line writes cost read-modify-write traffic in HBM
+    c->post_ld = (T + 31) / 32 * 32;
     c->post_rows = nlong;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
         c->n_cu = 256;
@@ -703,7 +706,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
                        (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
                        b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_diag, c->post_fast, idx,
-                       pn);
+                       pn, c->post_ld);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post kernels launch failed");
 }
 

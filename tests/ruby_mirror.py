@@ -81,6 +81,7 @@ class Corpus:
         ctx = ctypes.c_void_p()
         self._check(lib.dice_create(ctypes.byref(tpl), device, ctypes.byref(ctx)))
         self.ctx = ctx
+        self._setup_exact()
 
     def close(self):
         if self.ctx:
@@ -122,19 +123,62 @@ class Corpus:
                                                       best.ctypes.data, None, score.ctypes.data))
         return [(self.licenses[b], float(s)) if b >= 0 else (None, 0) for b, s in zip(best, score)]
 
+    def exact(self, files):
+        n = len(files)
+        if n == 0:
+            return []
+        out = np.empty(n, np.int32)
+        fmask = np.array([self._field_mask(f.wordset() or ()) for f in files], np.uint64)
+        fs = self._files_struct(files)
+        self._check(_native.load_library().dice_exact(self.ctx, ctypes.byref(fs), fmask.ctypes.data,
+                                                      out.ctypes.data))
+        return [self.licenses[i] if i >= 0 else None for i in out]
+
     def detect(self, license_files, threshold=98):
-        from licensee_amd.matchers import Copyright, Exact
+        from licensee_amd.matchers import Copyright
         out = [None] * len(license_files)
         rest = []
         for i, f in enumerate(license_files):
-            m = next((m for m in (k(f) for k in (Copyright, Exact)) if m.match() is not None), None)
-            if m is not None:
+            m = Copyright(f)
+            if m.match() is not None:
                 out[i] = (m.match(), m.confidence(), m.name)
             else:
                 rest.append(i)
-        for j, (license, confidence) in enumerate(self.match([license_files[i] for i in rest], threshold)):
-            out[rest[j]] = (license, confidence, 'dice') if license is not None else (License.find('other'), None, None)
+        files = [license_files[i] for i in rest]
+        exact = self.exact(files)
+        for j, (license, confidence) in enumerate(self.match(files, threshold)):
+            if exact[j] is not None:
+                out[rest[j]] = (exact[j], 100, 'exact')
+            elif license is not None:
+                out[rest[j]] = (license, confidence, 'dice')
+            else:
+                out[rest[j]] = (License.find('other'), None, None)
         return out
+
+    def _setup_exact(self):
+        self.fields = {}
+        t = len(self.licenses)
+        fbits = np.zeros(t * self.w64, np.uint64)
+        need = [0] * t
+        for i, l in enumerate(self.licenses):
+            words = l.fields_normalized_set()
+            self._put_bits(fbits, i, words)
+            for w in sorted(words):   # Ruby Set order is insertion order; any numbering works
+                if w in self.vocab:
+                    continue
+                k = self.fields.setdefault(w, len(self.fields))
+                if k >= 64:
+                    raise Error('more than 64 field words outside the vocabulary')
+                need[i] |= 1 << k
+        needp = np.array(need, np.uint64)
+        self._exact_keep = [fbits, needp]
+        ws = _u32([len(l.wordset()) for l in self.licenses])
+        self._exact_keep.append(ws)
+        self._check(_native.load_library().dice_exact_setup(self.ctx, ws.ctypes.data, fbits.ctypes.data,
+                                                            needp.ctypes.data))
+
+    def _field_mask(self, words):
+        return sum(1 << self.fields[w] for w in words if w in self.fields)
 
     def _files_struct(self, files):
         n = len(files)

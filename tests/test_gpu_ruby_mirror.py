@@ -116,6 +116,11 @@ def test_detect_equals_license_file_chain(corpus):
     texts = [c['normalized'] for t in golden('vendored.json')['templates'][:10] for c in t['cases'].values()]
     texts += ['Copyright (c) 2020 Foo Bar', 'not a license', '',
               'Attribution-NonCommercial 4.0\n' + License.find('cc-by-4.0').content_normalized()]
+    # Exact on the device (Corpus#exact): templates whose wordsets hold field words outside the
+    # vocabulary (ncsa, postgresql: 'fullname'), and the same texts with that word swapped out
+    for k in ('ncsa', 'postgresql', 'bsd-4-clause', 'vim'):
+        body = License.find(k).content_normalized()
+        texts += [body, body.replace('[fullname]', 'zzqxv').replace('[project]', 'zzqxw')]
     files = [LicenseFile(t, 'LICENSE') for t in texts]
     got = corpus.detect(files)
     kinds = set()

@@ -1,7 +1,7 @@
 """CPU check of the overlap bound the pruned match kernel uses (licensee_amd/csrc/dice_prune.hip).
 
-ov_t = |Lf_t ∩ W_F| is bounded by m_t = sum over 16 word groups g of min(A_g, F_g), with word
-group (p mod 64) / 4 of u64 word p. The kernel evaluates it as
+ov_t = |Lf_t ∩ W_F| is bounded by m_t = sum over G word groups g of min(A_g, F_g), with word
+group (p mod 64) / (64 / G) of u64 word p (G = 32 by default, 16 with DICE_PRUNE_GROUPS=16). The kernel evaluates it as
 (sum_g A'_g + sum_g F_g - sum_g |A'_g - F_g|) / 2 over byte-clamped A'_g = min(A_g, 255), which
 equals sum_g min(A_g, F_g) whenever every F_g <= 255 (else it uses m = |W_F ∩ V|). Checked here
 in numpy against the C oracle's exact overlaps (oracle/dice_ref.c, content_helper.rb:128-133):
@@ -10,14 +10,18 @@ the identity, the bound, and that the bound's score is an upper bound of the exa
 import numpy as np
 
 
-def _group_counts(bits):
+def _group_counts(bits, G=16):
     n, w64 = bits.shape
     per_word = np.unpackbits(bits.view(np.uint8), axis=1, bitorder='little').reshape(n, w64, 64).sum(2)
-    grp = (np.arange(w64) % 64) // 4
-    return np.stack([per_word[:, grp == g].sum(1) for g in range(16)], 1).astype(np.int64)
+    grp = (np.arange(w64) % 64) // (64 // G)
+    return np.stack([per_word[:, grp == g].sum(1) for g in range(G)], 1).astype(np.int64)
 
 
-def test_group_bound_identity_and_soundness():
+import pytest
+
+
+@pytest.mark.parametrize('G', [16, 32])
+def test_group_bound_identity_and_soundness(G):
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.license import License
     from licensee_amd.synth import SyntheticCorpus
@@ -27,8 +31,8 @@ def test_group_bound_identity_and_soundness():
     fb = SyntheticCorpus(c).generate(0, 2000, seed=131, nthreads=8)
     orc = OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
     mov, msc = orc.matrix(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, nthreads=8)
-    A = _group_counts(c.lf_bits)                  # [T, 16]
-    F = _group_counts(fb.bits)                    # [n, 16]
+    A = _group_counts(c.lf_bits, G)               # [T, G]
+    F = _group_counts(fb.bits, G)                 # [n, G]
     assert F.max() <= 255                         # synthetic license files stay on the byte path
     exact_min = np.minimum(A[None], F[:, None]).sum(2)
     A8 = np.minimum(A, 255)
