@@ -96,7 +96,7 @@ struct dice_ctx {
     void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
          *d_p4slot = nullptr, *d_p4orig = nullptr;
     int32_t p4_zkeep[2] = {-1, -1}, p4_zpos[2] = {0, 0};
-    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12, prune_gq = 2;
+    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12;
     int64_t prune_records = 0;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
     // two page-locked staging buffers for shard uploads from pageable caller memory

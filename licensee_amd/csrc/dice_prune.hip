@@ -771,22 +771,18 @@ struct Prune4Args {
     int32_t zpos[2];       // its position
 };
 
-template <int GQ, bool BIG, bool CC, bool CLAMP>
+template <bool BIG, bool CC, bool CLAMP>
 __device__ __forceinline__ uint32_t slot_key(const uint4* q8, const uint4* stc, const uint32_t* ccm, int32_t t,
-                                             uint32_t tag, int32_t T, bool pad, const uint32_t (&fb)[4 * GQ],
+                                             uint32_t tag, int32_t T, bool pad, const uint32_t (&fb)[4],
                                              uint32_t negwv, uint32_t m2big, uint32_t lf, uint32_t wf4) {
     const uint4 c = stc[t];
     uint32_t mm;
     if (!BIG) {
-        uint32_t d = negwv;
-#pragma unroll
-        for (int h = 0; h < GQ; ++h) {   // 16 group bytes per uint4
-            const uint4 a = q8[GQ * t + h];
-            d = __builtin_amdgcn_sad_u8(a.x, fb[4 * h + 0], d);
-            d = __builtin_amdgcn_sad_u8(a.y, fb[4 * h + 1], d);
-            d = __builtin_amdgcn_sad_u8(a.z, fb[4 * h + 2], d);
-            d = __builtin_amdgcn_sad_u8(a.w, fb[4 * h + 3], d);
-        }
+        const uint4 a = q8[t];
+        uint32_t d = __builtin_amdgcn_sad_u8(a.x, fb[0], negwv);
+        d = __builtin_amdgcn_sad_u8(a.y, fb[1], d);
+        d = __builtin_amdgcn_sad_u8(a.z, fb[2], d);
+        d = __builtin_amdgcn_sad_u8(a.w, fb[3], d);
         mm = c.w - d;
     } else {
         mm = m2big;
@@ -805,15 +801,15 @@ __device__ __forceinline__ uint32_t slot_key(const uint4* q8, const uint4* stc, 
 // template scored exactly, then the keys of every slot whose bound reaches the best score.
 // Returns with key[] filled (0 for skipped slots and the scored template) and llo / bi / bo / bd
 // set; first_scored false when slot jstar had no template with a nonzero bound.
-template <int GQ, int TJ, bool BIG, bool CC, bool CLAMP>
+template <int TJ, bool BIG, bool CC, bool CLAMP>
 __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, const uint32_t* ccm, const uint32_t* srec,
                                             const Prune4Args& pa, const uint64_t* myrow, int32_t T, int32_t jstar,
-                                            uint32_t sbk, const uint32_t (&fb)[4 * GQ], uint32_t negwv, uint32_t m2big,
+                                            uint32_t sbk, const uint32_t (&fb)[4], uint32_t negwv, uint32_t m2big,
                                             uint32_t lf, uint32_t wf, uint32_t wf4, bool fast, int lane,
                                             uint32_t (&key)[TJ], uint32_t& lane_max, float& llo, int32_t& bi,
                                             uint32_t& bo, int32_t& bd, PhaseClock& pclk) {
     const int32_t t0 = lane + jstar * kWave;
-    uint32_t ks = slot_key<GQ, BIG, CC, CLAMP>(q8, stc, ccm, t0, (uint32_t)(jstar + 1), T, (jstar + 1) * kWave > T, fb,
+    uint32_t ks = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, t0, (uint32_t)(jstar + 1), T, (jstar + 1) * kWave > T, fb,
                                            negwv, m2big, lf, wf4);
     __builtin_amdgcn_wave_barrier();   // the row (written above) is read by other lanes below
     const uint32_t K1 = rfl(__builtin_amdgcn_readlane(wave_incl_max(ks), kWave - 1));
@@ -840,7 +836,7 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
     for (int j = 0; j < TJ; ++j) {
         if (j == jstar) key[j] = ks;
         else if ((mask >> j) & 1)
-            key[j] = slot_key<GQ, BIG, CC, CLAMP>(q8, stc, ccm, lane + j * kWave, (uint32_t)(j + 1), T,
+            key[j] = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, lane + j * kWave, (uint32_t)(j + 1), T,
                                               j >= TJ - 2 && (j + 1) * kWave > T, fb, negwv, m2big, lf, wf4);
         else key[j] = 0;
         lane_max = max(lane_max, key[j]);
@@ -848,7 +844,7 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
     PHASE(4);
 }
 
-template <int J, int TJ, int NW, int GQ>
+template <int J, int TJ, int NW>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_prune4(
     const uint64_t* __restrict__ rows, int64_t n, int64_t per_wave, int32_t w64, int32_t T, Prune4Args pa,
     const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
@@ -863,22 +859,20 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     // address registers per slot) -- [kTP] uint4 group bytes | [kTP] uint4 constants | [kTP] cc
     // masks | [64] slot bounds | [kTP + 1] template index | record offset << 10 -- then the
     // waves' rows of J2 * 128 words
-    // (GQ uint4 of group bytes per template: 16 GQ word groups)
     extern __shared__ uint64_t lds[];
     uint4* q8 = reinterpret_cast<uint4*>(lds);
-    uint4* stc = q8 + kTP * GQ;
+    uint4* stc = q8 + kTP;
     uint32_t* ccm = reinterpret_cast<uint32_t*>(stc + kTP);
     uint4* ssb = reinterpret_cast<uint4*>(ccm + kTP);   // lanes >= TJ: empty slots
     uint32_t* srec = reinterpret_cast<uint32_t*>(ssb + kWave);
-    uint64_t* rows0 = lds + (((size_t)kTP * (16 * GQ + 20) + kWave * 16 + ((size_t)kTP + 1) * 4 + 15) / 16) * 2;
+    uint64_t* rows0 = lds + (((size_t)kTP * 36 + kWave * 16 + ((size_t)kTP + 1) * 4 + 15) / 16) * 2;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     uint64_t* myrow = rows0 + (size_t)wave * ((J + 1) / 2) * 2 * kWave;
     PhaseClock pclk;
     if (PRUNE3_DIAG & 8) pclk.init();
     for (int i = threadIdx.x; i < kTP; i += NW * kWave) {
-#pragma unroll
-        for (int h = 0; h < GQ; ++h) q8[GQ * i + h] = pa.q8[GQ * i + h];
+        q8[i] = pa.q8[i];
         stc[i] = pa.tc[i];
         ccm[i] = pa.ccm[i];
     }
@@ -941,27 +935,22 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
             deferred = true;
         } else {
             const uint32_t pc0 = pc;
-            // group counts: lane l's words are in group l / (4 / GQ); sum over the group's lanes
             pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-            if (GQ == 1) pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+            pc += (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
             const bool big = __ballot(pc > 255u) != 0;
-            uint32_t fb[4 * GQ];
-#pragma unroll
-            for (int k = 0; k < 4 * GQ; ++k) fb[k] = 0;
+            uint32_t fb[4] = {0, 0, 0, 0};
             uint32_t negwv = 0, m2big = 0, wv;
             if (!big) {
-                // four consecutive groups' bytes in one lane (DPP row shifts by one group), read
-                // from the lane of the last: 4 GQ readlanes
-                constexpr int S = 4 / GQ;   // lanes per group
                 uint32_t x = pc << 24;
-                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x110 + S, 0xf, 0xf, false) << 16;       // row_shr:S
-                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x110 + 2 * S, 0xf, 0xf, false) << 8;    // row_shr:2S
-                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x110 + 3 * S, 0xf, 0xf, false);         // row_shr:3S
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x114, 0xf, 0xf, false) << 16;   // row_shr:4
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x118, 0xf, 0xf, false) << 8;    // row_shr:8
+                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc, 0x11C, 0xf, 0xf, false);         // row_shr:12
 #pragma unroll
-                for (int k = 0; k < 4 * GQ; ++k) fb[k] = rfl(__builtin_amdgcn_readlane(x, 4 * S * k + 3 * S));
-                wv = 0;
-#pragma unroll
-                for (int k = 0; k < 4 * GQ; ++k) wv = __builtin_amdgcn_sad_u8(fb[k], 0u, wv);
+                for (int k = 0; k < 4; ++k) fb[k] = rfl(__builtin_amdgcn_readlane(x, 16 * k + 12));
+                wv = __builtin_amdgcn_sad_u8(fb[0], 0u, 0u);
+                wv = __builtin_amdgcn_sad_u8(fb[1], 0u, wv);
+                wv = __builtin_amdgcn_sad_u8(fb[2], 0u, wv);
+                wv = __builtin_amdgcn_sad_u8(fb[3], 0u, wv);
                 negwv = 0u - wv;
             } else {
                 wv = rfl(__builtin_amdgcn_readlane(wave_incl_scan(pc0), kWave - 1));
@@ -988,19 +977,19 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                 uint32_t key[TJ], lmax;
                 PHASE(1);
                 if (!big && !ccf && wf >= wf_noclamp)
-                    prune4_keys<GQ, TJ, false, false, false>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                    prune4_keys<TJ, false, false, false>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
                                                          lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else if (!big && !ccf)
-                    prune4_keys<GQ, TJ, false, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                    prune4_keys<TJ, false, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
                                                         lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else if (!big)
-                    prune4_keys<GQ, TJ, false, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                    prune4_keys<TJ, false, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
                                                        lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else if (!ccf)
-                    prune4_keys<GQ, TJ, true, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                    prune4_keys<TJ, true, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
                                                        lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 else
-                    prune4_keys<GQ, TJ, true, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
+                    prune4_keys<TJ, true, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
                 // the largest remaining key, scored while it can reach the best score (most files:
                 // no key is left at or above the best score, one compare per lane)
@@ -1101,10 +1090,10 @@ static int32_t prune3_j(int32_t w64) {
     return jw <= 2 ? jw : jw <= 4 ? 4 : jw <= 6 ? 6 : 8;
 }
 // v4: rows of ((J + 1) / 2) * 128 words, the v3 tables and the position -> template map
-static size_t prune4_lds_bytes(int32_t nw, int32_t w64, int32_t T, int32_t gq) {
+static size_t prune4_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
     const size_t tp = (size_t)prune3_tj(T) * kWave;
     return (size_t)nw * ((prune3_j(w64) + 1) / 2) * 2 * kWave * 8 +
-           (tp * (16 * gq + 16 + 4) + kWave * 16 + (tp + 1) * 4 + 15) / 16 * 16;
+           (tp * (16 + 16 + 4) + kWave * 16 + (tp + 1) * 4 + 15) / 16 * 16;
 }
 static size_t prune3_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
     const size_t tp = (size_t)prune3_tj(T) * kWave;
@@ -1123,27 +1112,25 @@ static int prune4_setup(dice_ctx* c, const dice_templates* t, const std::vector<
                         const std::vector<uint32_t>& qoff, const std::vector<uint4>& qrec) {
     const int32_t T = c->T;
     const size_t tp = (size_t)kPruneMaxT;
-    const int32_t G = 16 * c->prune_gq;   // word groups of the bound (16 or 32)
     std::vector<int32_t> pos2t((size_t)T);
     for (int32_t i = 0; i < T; ++i) pos2t[(size_t)i] = i;
     std::stable_sort(pos2t.begin(), pos2t.end(), [&](int32_t a, int32_t b) { return t->length[a] < t->length[b]; });
-    std::vector<uint32_t> q8p(tp * (size_t)G / 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0), srec(tp + 1, 0);
+    std::vector<uint32_t> q8p(tp * 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0), srec(tp + 1, 0);
     std::vector<uint4> tcp(tp, make_uint4(0, 0, 0, 0)), recp;
     recp.reserve(qrec.size());
     const int32_t w64 = c->w64;
     for (int32_t p = 0; p < T; ++p) {
         const int32_t i = pos2t[(size_t)p];
-        // group counts in v4's word groups: word w in group (w mod 64) / (64 / G) (8-byte row loads;
-        // ((w / 2) mod 64) / (64 / G) with 16-byte loads)
-        uint32_t gc[32] = {0};
+        // group counts in v4's word groups: word w in group ((w / 2) mod 64) / 4 (16-byte row loads)
+        uint32_t gc[kPruneGroups] = {0};
         const uint64_t* r = t->lf_bits + (size_t)i * w64;
         for (int32_t w = 0; w < w64; ++w)
-            gc[((P4_ROW16 ? w >> 1 : w) % kWave) / (kWave / G)] += (uint32_t)__builtin_popcountll(r[w]);
+            gc[((P4_ROW16 ? w >> 1 : w) % kWave) / (kWave / kPruneGroups)] += (uint32_t)__builtin_popcountll(r[w]);
         uint32_t sum8 = 0;
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < kPruneGroups; ++g) {
             const uint32_t a8 = std::min<uint32_t>(gc[g], 255u);
             sum8 += a8;
-            q8p[(size_t)p * (G / 4) + g / 4] |= a8 << (8 * (g % 4));
+            q8p[(size_t)p * 4 + g / 4] |= a8 << (8 * (g % 4));
         }
         tcp[(size_t)p] = tc3[(size_t)i];
         tcp[(size_t)p].w = sum8;
@@ -1208,7 +1195,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     if (e && *e == '0') return DICE_OK;
     const int32_t T = c->T, w64 = c->w64;
     if (T > kPruneMaxT || w64 > kPruneMaxJ * kWave || prune_lds_bytes(kPruneWaves, w64, T) > 160 * 1024 ||
-        prune4_lds_bytes(kPruneWaves, w64, T, 1) > 160 * 1024)
+        prune4_lds_bytes(kPruneWaves, w64, T) > 160 * 1024)
         return DICE_OK;
     // every table padded to the largest template count (704): each schedule reads its prefix.
     // Group counts A_g = |Lf_t ∩ g| clamped to bytes; the old and the v3 constants; the v3 CC
@@ -1279,11 +1266,6 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     // A/B: DICE_PRUNE_ROUTE_AT = exact scores before the routing test (v4; default 2)
     const char* ra = getenv("DICE_PRUNE_ROUTE_AT");
     if (ra && *ra) c->prune_route |= std::min(std::max(1, atoi(ra)), 64) << 16;
-    // bound word groups (v4): 32 (default) or 16; numpy simulation on 3000 config-3 files: deferred
-    // files 3.2% -> 0.63%, on long/mixed files 88% -> 45% (no group count above a byte: no coarse
-    // bound), mean exact scores per file 1.057 -> 1.021
-    const char* gr = getenv("DICE_PRUNE_GROUPS");
-    c->prune_gq = (gr && *gr && atoi(gr) == 16) || prune4_lds_bytes(kPruneWaves, w64, T, 2) > 160 * 1024 ? 1 : 2;
     const char* dg = diag_env("DICE_PRUNE_DIAG");
     c->prune_diag = dg && *dg ? atoi(dg) : 0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cu < 1)
@@ -1348,11 +1330,11 @@ static int launch_prune3(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) 
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune3 launch failed");
 }
 
-template <int J, int TJ, int GQ>
+template <int J, int TJ>
 static int launch_prune4(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     constexpr int NW = kPruneWaves;
-    const size_t lds = prune4_lds_bytes(NW, c->w64, c->T, GQ);
-    auto kern = dice_prune4<J, TJ, NW, GQ>;
+    const size_t lds = prune4_lds_bytes(NW, c->w64, c->T);
+    auto kern = dice_prune4<J, TJ, NW>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
     const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / NW, (160 * 1024) / (int64_t)lds));
@@ -1398,22 +1380,17 @@ static int launch_prune4(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) 
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune4 launch failed");
 }
 
-template <int J, int GQ>
-static int launch_prune4_tj(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    switch (prune3_tj(c->T)) {
-        case 2: return launch_prune4<J, 2, GQ>(c, b, thr, s);
-        case 4: return launch_prune4<J, 4, GQ>(c, b, thr, s);
-        case 6: return launch_prune4<J, 6, GQ>(c, b, thr, s);
-        case 8: return launch_prune4<J, 8, GQ>(c, b, thr, s);
-        case 10: return launch_prune4<J, 10, GQ>(c, b, thr, s);
-        default: return launch_prune4<J, (kPruneMaxT + kWave - 1) / kWave, GQ>(c, b, thr, s);
-    }
-}
-
 template <int J>
 static int launch_prune3_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     if (c->prune_sched != 6 && (!P4_ROW16 || (c->w64 & 1) == 0)) {   // v4 (16-byte row loads: even w64) unless v3
-        return c->prune_gq == 1 ? launch_prune4_tj<J, 1>(c, b, thr, s) : launch_prune4_tj<J, 2>(c, b, thr, s);
+        switch (prune3_tj(c->T)) {
+            case 2: return launch_prune4<J, 2>(c, b, thr, s);
+            case 4: return launch_prune4<J, 4>(c, b, thr, s);
+            case 6: return launch_prune4<J, 6>(c, b, thr, s);
+            case 8: return launch_prune4<J, 8>(c, b, thr, s);
+            case 10: return launch_prune4<J, 10>(c, b, thr, s);
+            default: return launch_prune4<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
+        }
     }
     switch (prune3_tj(c->T)) {
         case 2: return launch_prune3<J, 2>(c, b, thr, s);

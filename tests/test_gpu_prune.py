@@ -119,24 +119,6 @@ def _random_files(c, n, seed, density):
     return FileBatch(bits, wf, ln, cc)
 
 
-@pytest.mark.parametrize('groups', ['16', '32'])
-def test_bound_word_groups(config3, groups, monkeypatch):
-    """The bound over 16 or 32 vocabulary word groups (DICE_PRUNE_GROUPS; 32 is the default):
-    config-3 files, random files (loose bounds, deferral) and dense files (group counts near
-    a byte) bit-exact against the oracle and the postings kernel."""
-    from licensee_amd._native import FileBatch
-    monkeypatch.setenv('DICE_PRUNE_GROUPS', groups)
-    c, fb = config3
-    rnd = _random_files(c, 1500, seed=11, density=0.05)
-    dense = _random_files(c, 300, seed=12, density=0.6)
-    sub = slice(0, 8000)
-    both = FileBatch(np.concatenate([fb.bits[sub], rnd.bits, dense.bits]),
-                     np.concatenate([fb.wordset_size[sub], rnd.wordset_size, dense.wordset_size]),
-                     np.concatenate([fb.length[sub], rnd.length, dense.length]),
-                     np.concatenate([fb.cc_false_positive[sub], rnd.cc_false_positive, dense.cc_false_positive]))
-    _check(c, both, monkeypatch)
-
-
 @pytest.mark.parametrize('max_evals', ['8', '0', '1'])
 def test_files_resembling_nothing(config3, max_evals, monkeypatch):
     """Loose bounds: with deferral (DICE_PRUNE_MAX_EVALS, default 8; 1 defers every file that

@@ -1,7 +1,8 @@
 """CPU check of the overlap bound the pruned match kernel uses (licensee_amd/csrc/dice_prune.hip).
 
 ov_t = |Lf_t ∩ W_F| is bounded by m_t = sum over G word groups g of min(A_g, F_g), with word
-group (p mod 64) / (64 / G) of u64 word p (G = 32 by default, 16 with DICE_PRUNE_GROUPS=16). The kernel evaluates it as
+group (p mod 64) / (64 / G) of u64 word p (the kernel uses G = 16; G = 32, measured as an A/B in
+round 3, is checked too). The kernel evaluates it as
 (sum_g A'_g + sum_g F_g - sum_g |A'_g - F_g|) / 2 over byte-clamped A'_g = min(A_g, 255), which
 equals sum_g min(A_g, F_g) whenever every F_g <= 255 (else it uses m = |W_F ∩ V|). Checked here
 in numpy against the C oracle's exact overlaps (oracle/dice_ref.c, content_helper.rb:128-133):
