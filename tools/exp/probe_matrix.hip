@@ -58,8 +58,12 @@ __device__ __forceinline__ int qidx(int i) {
     return (i & 1) ? (i >> 1) : WQ - 1 - (i >> 1);
 }
 
-template <int WQ, int B, int ORDER>
+template <int WQ, int B, int ORDER, int PADKB = 0>
 __global__ __launch_bounds__(256) void bursts(const uint4* __restrict__ f, long ntiles, uint32_t* __restrict__ out) {
+    // PADKB: LDS per workgroup only to cap the occupancy (40 KB: 4 workgroups = 4 waves per SIMD,
+    // the sparse program's)
+    __shared__ uint32_t pad[PADKB > 0 ? PADKB * 256 : 1];
+    if (PADKB > 0 && threadIdx.x == 0 && ntiles < 0) pad[0] = 0;
     const int lane = threadIdx.x & 63;
     const long tile = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= ntiles) return;
@@ -84,22 +88,90 @@ __global__ __launch_bounds__(256) void bursts(const uint4* __restrict__ f, long 
     if (x == 0x12345678u) out[tile * 64 + lane] = x;
 }
 
-template <int B, int ORDER>
-static void time_bursts(const uint4* f, long ntiles, uint32_t* out, long n) {
+// LDS-DMA on top of the VGPR bursts: the first L quads of the tile go straight to a per-wave LDS
+// buffer (global_load_lds_dwordx4: no VGPRs), so 2B + L quads are in flight at the start; the VGPR
+// bursts then cover the rest. (40 KB of LDS per workgroup in total: 4 waves per SIMD.)
+__device__ __forceinline__ void dma16(const uint4* src, uint4* dst) {
+    __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WQ, int B, int L>
+__global__ __launch_bounds__(256) void bursts_lds(const uint4* __restrict__ f, long ntiles, uint32_t* __restrict__ out) {
+    __shared__ uint4 buf[4][L > 0 ? L : 1][64];
+    __shared__ uint32_t pad[(40 * 256 - 4 * (L > 0 ? L : 1) * 64 * 4) > 0 ? (40 * 256 - 4 * (L > 0 ? L : 1) * 64 * 4) : 1];
+    if (threadIdx.x == 0 && ntiles < 0) pad[0] = 0;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const long tile = (long)blockIdx.x * 4 + w;
+    if (tile >= ntiles) return;
+    const uint4* p = f + tile * WQ * 64 + lane;
+#pragma unroll
+    for (int j = 0; j < L; ++j) dma16(p + j * 64, &buf[w][j][0]);
+    constexpr int R = WQ - L;
+    constexpr int NB = (R + B - 1) / B;
+    u32x4 cur[B], nxt[B];
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < B; ++j) cur[j] = j < R ? __builtin_nontemporal_load((const u32x4*)(p + (L + j) * 64)) : u32x4{0, 0, 0, 0};
+    wait_vm<B>();   // the L DMAs (issued first) landed
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const uint4 v = buf[w][j][lane];
+        x += v.x ^ v.y ^ v.z ^ v.w;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const int i = (b + 1) * B + j;
+            nxt[j] = i < R ? __builtin_nontemporal_load((const u32x4*)(p + (L + i) * 64)) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) x += cur[j].x ^ cur[j].y ^ cur[j].z ^ cur[j].w;
+#pragma unroll
+        for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+    }
+    if (x == 0x12345678u) out[tile * 64 + lane] = x;
+}
+
+template <int B, int L>
+static void time_bursts_lds(const uint4* f, long ntiles, uint32_t* out, long n) {
     const dim3 grid((unsigned)((ntiles + 3) / 4)), block(256);
-    for (int w = 0; w < 5; ++w) bursts<28, B, ORDER><<<grid, block>>>(f, ntiles, out);
+    for (int w = 0; w < 5; ++w) bursts_lds<28, B, L><<<grid, block>>>(f, ntiles, out);
     CK(hipDeviceSynchronize());
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     CK(hipEventRecord(a));
-    for (int r = 0; r < 50; ++r) bursts<28, B, ORDER><<<grid, block>>>(f, ntiles, out);
+    for (int r = 0; r < 50; ++r) bursts_lds<28, B, L><<<grid, block>>>(f, ntiles, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
     const double us = ms * 1e3 / 50;
-    printf("bursts of %d, order %d: %.1f us, %.2f TB/s\n", B, ORDER, us, n * 448.0 / (us * 1e-6) / 1e12);
+    printf("bursts of %d + %d quads by LDS-DMA (4 waves/SIMD): %.1f us, %.2f TB/s\n", B, L, us, n * 448.0 / (us * 1e-6) / 1e12);
+}
+
+template <int B, int ORDER, int PADKB = 0>
+static void time_bursts(const uint4* f, long ntiles, uint32_t* out, long n) {
+    const dim3 grid((unsigned)((ntiles + 3) / 4)), block(256);
+    for (int w = 0; w < 5; ++w) bursts<28, B, ORDER, PADKB><<<grid, block>>>(f, ntiles, out);
+    CK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    for (int r = 0; r < 50; ++r) bursts<28, B, ORDER, PADKB><<<grid, block>>>(f, ntiles, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const double us = ms * 1e3 / 50;
+    printf("bursts of %d, order %d, lds pad %d KB: %.1f us, %.2f TB/s\n", B, ORDER, PADKB, us, n * 448.0 / (us * 1e-6) / 1e12);
 }
 
 int main() {
@@ -140,6 +212,13 @@ int main() {
         printf("%s: %.1f us per launch, %.2f TB/s of %.0f MB\n", mode ? "read + matrix writes" : "read only", us,
                bytes / (us * 1e-6) / 1e12, bytes / 1e6);
     }
+    time_bursts<5, 1, 40>(f, ntiles, ov, n);
+    time_bursts<7, 1, 40>(f, ntiles, ov, n);
+    time_bursts<28, 0, 40>(f, ntiles, ov, n);
+    time_bursts_lds<5, 0>(f, ntiles, ov, n);
+    time_bursts_lds<5, 4>(f, ntiles, ov, n);
+    time_bursts_lds<5, 8>(f, ntiles, ov, n);
+    time_bursts_lds<5, 10>(f, ntiles, ov, n);
     time_bursts<3, 0>(f, ntiles, ov, n);
     time_bursts<5, 0>(f, ntiles, ov, n);
     time_bursts<5, 1>(f, ntiles, ov, n);
