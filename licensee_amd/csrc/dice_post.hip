@@ -316,6 +316,13 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
                                              int32_t* __restrict__ tki, double* __restrict__ tks, int lane) {
     int32_t bi = -1, bd = 1;
     uint32_t bo = 0;
+    // the file's row bases (wave-uniform) and the lane's offset: every store of the unrolled loop
+    // is base + lane offset + an immediate (< 4 KiB: the score row restarts at template 320), so
+    // no per-template 64-bit address stays live (they spilled, and each scratch reload's
+    // vmcnt(0) waited for every store issued before it)
+    uint32_t* orow = kMatrix ? mov + file * ld : nullptr;
+    double* srow0 = kMatrix ? msc + file * ld : nullptr;
+    double* srow1 = srow0 + 5 * kWave;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
         const int32_t t = lane + j * kWave;
@@ -324,8 +331,8 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             int32_t den;
             lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             if (kMatrix) {
-                __builtin_nontemporal_store(ov, &mov[file * ld + t]);
-                __builtin_nontemporal_store(dice_score(ov, den), &msc[file * ld + t]);
+                __builtin_nontemporal_store(ov, &orow[t]);
+                __builtin_nontemporal_store(dice_score(ov, den), j < 5 ? &srow0[t] : &srow1[t - 5 * kWave]);
             }
         }
     }
