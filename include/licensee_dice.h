@@ -197,7 +197,8 @@ int64_t dice_batch_bytes_per_file(const dice_batch *batch);
  * licensee_host.h lh_template_field_masks). Per file, file_field_mask[i] (host, [n]; NULL =
  * all zero) holds the same numbering's bits of the file's wordset (lh_prep_files).
  * exact[i] = template index or -1. The kernel reads the batch's row-major bitsets (the
- * stream probe overwrites them). dice_batch_exact is asynchronous on `stream`. */
+ * stream probe overwrites them). dice_batch_exact is asynchronous on `stream`: the field masks
+ * are copied from host memory on that stream, so they must stay valid until it has run. */
 int dice_exact_setup(dice_ctx *ctx, const uint32_t *wordset_size, const uint64_t *field_bits,
                      const uint64_t *field_need);
 int dice_batch_exact(dice_batch *batch, const uint64_t *file_field_mask, void *stream);
