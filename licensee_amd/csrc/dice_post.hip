@@ -479,10 +479,19 @@ __device__ __forceinline__ void post_narrow_body(
         const uint64_t* row = rows + file * w64;
         // this file's dense partials start its counter row (a plain copy, u16 pairs widened: the
         // row is zero here and this wave's postings adds come after it)
+        if (!kMatrix) {
+            // one LDS address and immediate offsets: the match kernel then spills nothing (4 VGPRs
+            // before); the matrix kernel allocates better with per-j addresses
+            uint2* dst = reinterpret_cast<uint2*>(crow32) + lane;
 #pragma unroll
-        for (int j = 0; j < kPJ; ++j) {
-            const int32_t i = lane + j * kWave;
-            if (i < tp / 2) *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
+            for (int j = 0; j < kPJ; ++j)
+                if (lane + j * kWave < tp / 2) dst[j * kWave] = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPJ; ++j) {
+                const int32_t i = lane + j * kWave;
+                if (i < tp / 2) *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
+            }
         }
         const uint32_t wf = rfl(__builtin_amdgcn_readlane(twf, fi));
         const int32_t lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
