@@ -495,6 +495,26 @@ def main():
     if rank == 0 and not matrix_mode and not args.probe and not args.no_extras:
         torch.cuda.synchronize()
         extras['single_file_us'] = single_file_latency(run)
+        # Exact#match on the device over the resident batch (dice_batch_exact; the synthetic files
+        # hold no template field words: all-zero field masks)
+        from licensee_amd.batch import exact_tables
+        from licensee_amd.native_host import HostPrep
+        run.scorer.exact_setup(*exact_tables(corpus, HostPrep(corpus)))
+        batch.upload(files, sptr)
+        fm = np.zeros(n_per, np.uint64)
+        batch.exact(fm, sptr)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            batch.exact(None, sptr)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ex = batch.download_exact(sptr)
+        extras['exact_kernel'] = {'launch_us': e0.elapsed_time(e1) / 20 * 1e3, 'files': n_per,
+                                  'exact_matches': int((ex >= 0).sum()),
+                                  'note': 'dice_batch_exact over the resident batch (kernel only, no field-mask '
+                                          'upload): Exact#match for every file beside the Dice pass'}
 
     cpu_baseline = None
     parity = None

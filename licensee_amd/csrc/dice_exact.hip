@@ -12,9 +12,10 @@
 // both are impossible: Lf_t ⊆ V.
 //
 // Kernel: one lane per file. The templates are sorted by (|W_t|, key index) on the host; a
-// lane binary-searches |W_F| among the sorted sizes (in LDS) and checks the few templates of
-// that size in key order -- most files have none, so the pass reads 4 B (|W_F|) + 8 B (field
-// mask) and writes 4 B per file, plus the row words of the rare size-equal candidates.
+// lane binary-searches |W_F| among the sorted sizes (in LDS); the few templates of that size are
+// checked in key order by the whole wave, one (file, template) pair at a time -- most files have
+// none, so the pass reads 4 B (|W_F|) + 8 B (field mask) and writes 4 B per file, plus the row
+// words of the size-equal candidates.
 #include <algorithm>
 #include <string>
 #include <vector>
@@ -26,7 +27,11 @@ namespace dice {
 
 namespace {
 
-// sorted position k: {|W_t|, t, first record, end record}
+// sorted position k: {|W_t|, t, first record, end record}. One lane per file finds its size-equal
+// templates (binary search over the sizes in LDS); the wave then checks the pending (file,
+// template) pairs one at a time with all 64 lanes -- lanes = the template's records (coalesced
+// 1 KiB loads), each reading its word of that one file's row -- so a pair costs two dependent
+// loads instead of a record loop in one lane while the other 63 wait.
 __global__ __launch_bounds__(256) void dice_exact_kernel(const uint64_t* __restrict__ rows, int64_t n, int32_t w64,
                                                          const uint32_t* __restrict__ wf,
                                                          const uint64_t* __restrict__ fmask,
@@ -37,35 +42,52 @@ __global__ __launch_bounds__(256) void dice_exact_kernel(const uint64_t* __restr
     extern __shared__ uint32_t sz[];
     for (int i = threadIdx.x; i < T; i += blockDim.x) sz[i] = tbl[i].x;
     __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= n) return;
-    const uint32_t w = wf[f];
+    const bool valid = f < n;
+    const uint32_t w = valid ? wf[f] : 0xFFFFFFFFu;
     int32_t lo = 0, hi = T;
     while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
         if (sz[mid] < w) lo = mid + 1;
         else hi = mid;
     }
+    const uint64_t fm = valid && fmask ? fmask[f] : 0ull;
     int32_t res = -1;
-    if (lo < T && sz[lo] == w) {
-        const uint64_t fm = fmask ? fmask[f] : 0ull;
-        const uint64_t* row = rows + f * (int64_t)w64;
-        for (int32_t k = lo; k < T && sz[k] == w; ++k) {
-            if ((need[k] & ~fm) != 0) continue;
-            const uint4 e = tbl[k];
-            bool ok = true;
-            for (uint32_t r = e.z; r < e.w && ok; ++r) {
+    int32_t kc = valid && lo < T && sz[lo] == w ? lo : -1;   // this lane's next candidate position
+    // skip candidates whose non-vocabulary field words the file lacks (lane-local)
+    while (kc >= 0 && (need[kc] & ~fm) != 0) kc = kc + 1 < T && sz[kc + 1] == w ? kc + 1 : -1;
+    for (uint64_t pend = __ballot(kc >= 0); pend; pend = __ballot(kc >= 0)) {
+        const int src = (int)__builtin_ctzll(pend);
+        const int32_t k = __builtin_amdgcn_readlane(kc, src);
+        const int64_t fs = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~(kWave - 1)) + src;
+        const uint64_t* row = rows + fs * (int64_t)w64;
+        const uint4 e = tbl[k];
+        bool ok = true;
+        for (uint32_t r0 = e.z; r0 < e.w; r0 += kWave) {
+            const uint32_t r = r0 + (uint32_t)lane;
+            bool bad = false;
+            if (r < e.w) {
                 const uint4 q = rec[r];
                 const uint64_t m = (uint64_t)q.y | ((uint64_t)q.z << 32);
-                ok = (row[q.x] & m) == m;
+                bad = (row[q.x] & m) != m;
             }
-            if (ok) {
-                res = (int32_t)e.y;
+            if (__ballot(bad)) {
+                ok = false;
                 break;
             }
         }
+        if (lane == src) {
+            if (ok) {
+                res = (int32_t)e.y;
+                kc = -1;
+            } else {
+                do kc = kc + 1 < T && sz[kc + 1] == w ? kc + 1 : -1;
+                while (kc >= 0 && (need[kc] & ~fm) != 0);
+            }
+        }
     }
-    out[f] = res;
+    if (valid) out[f] = res;
 }
 
 struct Guard {
