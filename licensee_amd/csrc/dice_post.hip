@@ -308,6 +308,9 @@ __device__ __forceinline__ void lane_best(const uint32_t* crow32, const uint2* t
     }
 }
 
+#ifndef POST_MATRIX_STORE
+#define POST_MATRIX_STORE 3
+#endif
 template <bool kMatrix, int TJ, bool FAST>
 __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs, int32_t T, int32_t ld, int64_t file, uint32_t wf,
                                              int32_t lf, bool cc, double thr, int32_t* __restrict__ best_out,
@@ -331,8 +334,18 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             int32_t den;
             lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             if (kMatrix) {
-                __builtin_nontemporal_store(ov, &orow[t]);
-                __builtin_nontemporal_store(dice_score(ov, den), j < 5 ? &srow0[t] : &srow1[t - 5 * kWave]);
+                const double sc = dice_score(ov, den);
+                double* sp = j < 5 ? &srow0[t] : &srow1[t - 5 * kWave];
+                // diagnostics (POST_MATRIX_STORE, A/B builds only): bit 0 / 1 store overlaps / scores
+                // (a cleared bit still computes them), bit 2 plain stores instead of nontemporal
+                if ((POST_MATRIX_STORE & 1) || ov == 0xFFFFFFFFu) {
+                    if (POST_MATRIX_STORE & 4) orow[t] = ov;
+                    else __builtin_nontemporal_store(ov, &orow[t]);
+                }
+                if ((POST_MATRIX_STORE & 2) || ov == 0xFFFFFFFFu) {
+                    if (POST_MATRIX_STORE & 4) *sp = sc;
+                    else __builtin_nontemporal_store(sc, sp);
+                }
             }
         }
     }
