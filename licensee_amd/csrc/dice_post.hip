@@ -334,6 +334,10 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             int32_t den;
             lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             if (kMatrix) {
+#if POST_MATRIX_STORE == 3
+                __builtin_nontemporal_store(ov, &orow[t]);
+                __builtin_nontemporal_store(dice_score(ov, den), j < 5 ? &srow0[t] : &srow1[t - 5 * kWave]);
+#else
                 const double sc = dice_score(ov, den);
                 double* sp = j < 5 ? &srow0[t] : &srow1[t - 5 * kWave];
                 // diagnostics (POST_MATRIX_STORE, A/B builds only): bit 0 / 1 store overlaps / scores
@@ -346,6 +350,7 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
                     if (POST_MATRIX_STORE & 4) *sp = sc;
                     else __builtin_nontemporal_store(sc, sp);
                 }
+#endif
             }
         }
     }
