@@ -7,23 +7,29 @@ LICENSE files per GPU scored against the 47 vendored choosealicense.com template
 (Dice#match with the default threshold 98). Files are generated in normalized space
 (licensee_amd/csrc/synth.cpp), interned to bitsets, uploaded once and stay resident in HBM;
 a step is one dice_batch_match launch over the whole batch (inputs and results in HBM).
-For N > 1 (torch.distributed.run, one rank per GPU) each rank scores its own disjoint
-1M-file shard -- no data-path collective, "scaling": "weak"; results are gathered once
-after the timed region (host D2H and RCCL all_gather both timed, reported as extras).
+For N > 1 one process per GPU: `python bench.py --gpus N` starts the N ranks itself (a child
+torch.distributed.run on 127.0.0.1, before any GPU call in this process) and relays rank 0's
+line; under an external torch.distributed.run it runs as one of the ranks (WORLD_SIZE must equal
+--gpus). Each rank scores its own disjoint 1M-file shard -- no data-path collective, "scaling":
+"weak"; results are gathered once after the timed region (host D2H and RCCL all_gather both
+timed, the faster reported as gather_winner). RCCL (backend nccl) when every rank has its own
+device; gloo when ranks share one (the one-GPU box's rehearsal of the N > 1 path).
 
 The JSON line also carries:
   roofline     -- algorithmic bytes per launch (tile bitset + |W_F| + len + cc + 16 B of
                   results per file) / average launch duration from HIP events on the launch
                   stream; peak 8000 GB/s (MI355X HBM3E). traffic = per-launch HBM bytes from
                   the committed rocprofv3 PMC pass (profiles/pmc_<config>.json) when present.
-  cpu_baseline -- oracle/dice_ref.c (C port of the reference Set#& algorithm), rank 0 at N=1,
-                  on a bounded sample of the same files, on every core the process may use.
-  parity       -- GPU results of the timed run vs the C oracle's hash mode on that sample.
-  extras.configs -- at N=1, the other BASELINE configs (3: ~600 templates, bound-pruned match
+  cpu_baseline -- oracle/dice_ref.c (C port of the reference Set#& algorithm), rank 0, on a
+                  bounded sample of its own shard, on every core the process may use (the other
+                  ranks wait meanwhile).
+  parity       -- GPU results of the timed run vs the C oracle's hash mode: every rank checks a
+                  sample of its own shard; checked files and mismatches are summed over ranks.
+  extras.configs -- the other BASELINE configs (3: ~600 templates, bound-pruned match
                   kernel, plus '3-allpairs': the same files on the postings kernel, which scores
                   every pair; 4: long/mixed files; 5: full matrix + top-k) measured in the same
-                  run, each with its own HIP-event launch time, roofline fraction and oracle
-                  parity sample.
+                  run (every rank, its own shard), each with its own HIP-event launch time, roofline
+                  fraction, cpu_baseline and oracle parity sample.
 """
 from __future__ import annotations
 
@@ -181,19 +187,54 @@ class Run:
         self.scorer, self.batch, self.match_kernel = saved
 
 
-def timed(run, steps, warmup, stream, distributed):
+class Group:
+    """The ranks of this run (world 1: no-ops). Collectives go over the process group's backend:
+    RCCL with device tensors, or gloo with host tensors when ranks share a device."""
+
+    def __init__(self, rank=0, world=1, backend=None):
+        self.rank, self.world, self.backend = rank, world, backend
+
+    def _t(self, vals, dtype):
+        import torch
+        return torch.tensor(vals, dtype=dtype, device='cuda' if self.backend == 'nccl' else 'cpu')
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def reduce(self, vals, op='max'):
+        """Element-wise max or sum of a list of floats over the ranks."""
+        if self.world == 1:
+            return list(vals)
+        import torch
+        import torch.distributed as dist
+        t = self._t(vals, torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 'max' else dist.ReduceOp.SUM)
+        return [float(x) for x in t.cpu()]
+
+    def bcast(self, val):
+        """Rank 0's integer to every rank."""
+        if self.world == 1:
+            return val
+        import torch
+        import torch.distributed as dist
+        t = self._t([int(val)], torch.int64)
+        dist.broadcast(t, 0)
+        return int(t.cpu()[0])
+
+
+def timed(run, steps, warmup, stream, group):
     """W untimed steps, then K steps between barrier + synchronize; HIP events on the launch
     stream give the per-launch time; wall time and event time are max-reduced over ranks."""
     import torch
-    import torch.distributed as dist
     sptr = stream.cuda_stream
     run.batch.upload(run.files, sptr)
     torch.cuda.synchronize()
     for _ in range(warmup):
         run.step(sptr)
     torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
+    group.barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -203,18 +244,31 @@ def timed(run, steps, warmup, stream, distributed):
         run.step(sptr)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
+    group.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
     ev_ms = ev0.elapsed_time(ev1)
-    if distributed:
-        t = torch.tensor([wall, ev_ms], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, ev_ms = float(t[0]), float(t[1])
+    wall, ev_ms = group.reduce([wall, ev_ms], 'max')
     launch_ms = ev_ms / steps
     achieved = run.algo_bytes_per_file * run.n_per / (launch_ms * 1e-3) / 1e9
     return wall, launch_ms, achieved
+
+
+def staged_parity(group, check):
+    """Every rank's oracle parity check of its own shard, rank 0 first while the others wait (so
+    rank 0's oracle time -- the cpu_baseline -- runs on an otherwise idle host), then the rest
+    together. check() -> dict with checked_files, mismatches, oracle[, oracle_files_per_s].
+    Returns rank 0's dict with checked_files / mismatches summed over the ranks."""
+    res = check() if group.rank == 0 else None
+    group.barrier()
+    if group.rank != 0:
+        res = check()
+    group.barrier()
+    tot = group.reduce([res['checked_files'], res['mismatches']], 'sum')
+    res['checked_files'], res['mismatches'] = int(tot[0]), int(tot[1])
+    if group.world > 1:
+        res['ranks_checked'] = group.world
+    return res
 
 
 def oracle_for(corpus):
@@ -322,32 +376,61 @@ def single_file_latency(run, n_calls=400):
     return out
 
 
-def measure_extra(r, c, args, stream, sptr, cpu):
+def measure_extra(r, c, args, stream, sptr, cpu, group):
     steps = min(args.steps, 20)
-    w, lm, ach = timed(r, steps, 2, stream, False)
+    w, lm, ach = timed(r, steps, 2, stream, group)
     tr, tr_src = traffic_for(c if c != '5-T600' else '5_T600', r.n_per, r.T,
                              '_post' if (c == 3 and r.match_kernel == 3) else '')
-    rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'templates': r.T, 'vocab': r.V,
-           'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': r.n_per * steps / w,
-           'scores_per_s': r.n_per * steps / w * r.T, 'launch_ms': lm,
+    files = r.n_per * group.world
+    rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'global_files': files, 'templates': r.T,
+           'vocab': r.V, 'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': files * steps / w,
+           'scores_per_s': files * steps / w * r.T, 'launch_ms': lm,
            'algorithmic_bytes_per_file': r.algo_bytes_per_file, 'roofline_achieved_gbs': ach,
            'roofline_frac': ach / HBM_PEAK_GBS, 'traffic': tr, 'traffic_source': tr_src}
     if r.match_kernel == 4:
         rec['note'] = ('bound-pruned Dice#match: every (file, template) pair is decided, but only pairs whose '
                        'overlap bound can reach the top score are scored exactly (DESIGN.md 4); scores_per_s '
                        'counts decided pairs. 3-allpairs scores every pair')
-        rec['deferred_files'] = r.batch.deferred(sptr)
+        rec['deferred_files'] = int(group.reduce([r.batch.deferred(sptr)], 'sum')[0])
     if not args.no_cpu_baseline:
-        rec['parity'] = parity_sample(r, oracle_for(r.corpus), sptr, cpu['threads'],
-                                      {3: 20_000, 4: 30_000, 5: 50_000, '5-T600': 10_000}[c])
-        # the parity leg is the reference-equivalent CPU path on the same files: its rate
-        rec['cpu_baseline'] = {'value': rec['parity'].pop('oracle_files_per_s'), 'unit': 'files/s',
+        n_sample = {3: 20_000, 4: 30_000, 5: 50_000, '5-T600': 10_000}[c]
+        threads = cpu['threads'] if group.rank == 0 else cpu['rank_threads']
+        par = staged_parity(group, lambda: parity_sample(r, oracle_for(r.corpus), sptr, threads, n_sample))
+        # rank 0's parity leg is the reference-equivalent CPU path on its own files: its rate
+        rec['cpu_baseline'] = {'value': par.pop('oracle_files_per_s'), 'unit': 'files/s',
                                'cores': cpu['threads'], 'kind': 'port',
-                               'sample': f"the parity sample: first {rec['parity']['checked_files']} files, "
-                                         f"hash-set Set#& restatement (oracle/dice_ref.c)"}
-    log(f"config {c} ({rec['kernel']}): {rec['files_per_s']:.3e} files/s, launch {lm * 1e3:.1f} us, "
-        f"frac {rec['roofline_frac']:.3f}, parity {rec.get('parity')}")
+                               'sample': f"rank 0's parity sample: first {min(n_sample, r.n_per)} files of its "
+                                         f"shard, hash-set Set#& restatement (oracle/dice_ref.c)"}
+        rec['parity'] = par
+    if group.rank == 0:
+        log(f"config {c} ({rec['kernel']}): {rec['files_per_s']:.3e} files/s, launch {lm * 1e3:.1f} us, "
+            f"frac {rec['roofline_frac']:.3f}, parity {rec.get('parity')}")
     return rec
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n, argv, script=None):
+    """`bench.py --gpus N` with no RANK in the environment: start the N ranks as a child
+    torch.distributed.run (this process makes no GPU call, so nothing is initialized before the
+    children exist) and relay rank 0's JSON line. Returns the children's exit code."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr=127.0.0.1', f'--master-port={free_port()}', script or os.path.abspath(__file__)] + argv
+    log('self-launch:', ' '.join(cmd))
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    if lines:
+        sys.stdout.write(lines[-1] + '\n')
+        sys.stdout.flush()
+    return p.returncode if lines or p.returncode else 1
 
 
 def main():
@@ -364,6 +447,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--extra-configs', default='3,4,5,5-T600',
                     help="configs also measured at N=1 (reported under extras.configs); '' for none")
+    ap.add_argument('--extra-files-per-gpu', type=int, default=None,
+                    help='files per GPU of the extra configs (default: each config\'s BASELINE size)')
     ap.add_argument('--probe', action='store_true', help='diagnostic: stream-read the tiles only (read ceiling)')
     ap.add_argument('--corpus', default='synthetic', choices=['synthetic', 'spdx'],
                     help="config 3's templates: synthetic, or the 94 real texts (47 choosealicense.com + 47 SPDX "
@@ -372,6 +457,9 @@ def main():
                     help='skip the separately reported host-side rates (PCIe end-to-end, host prep, single-file '
                          'calls): profiling runs then trace only the timed workload')
     args = ap.parse_args()
+
+    if args.gpus > 1 and 'RANK' not in os.environ:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
 
     # stdout carries exactly one JSON line: anything native libraries print there (RCCL's
     # version banner at communicator init, for one) is sent to stderr instead.
@@ -386,15 +474,32 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     distributed = 'RANK' in os.environ and 'MASTER_PORT' in os.environ   # launched by torch.distributed.run
+    if distributed and world != args.gpus:
+        raise SystemExit(f'bench.py: WORLD_SIZE={world} but --gpus {args.gpus}')
+    group = Group()
+    n_dev = torch.cuda.device_count()            # counts devices without initializing HIP
     if distributed:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+        dev_index = local_rank % max(n_dev, 1)
+        torch.cuda.set_device(dev_index)
+        # RCCL needs one device per rank; ranks sharing a device (the one-GPU box rehearsing N > 1)
+        # coordinate over gloo instead. Neither carries data-path traffic.
+        backend = 'nccl' if n_dev >= local_world else 'gloo'
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_index))
+        else:
+            dist.init_process_group('gloo')
+        group = Group(rank, world, backend)
     else:
+        local_world = 1
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
     cpu = cpu_info()
-    nthreads = min(16, cpu['threads'])            # generator / host-prep threads (box CPU share)
+    # host threads of one rank: every core for rank 0's timed CPU baseline; a 1/local_world share
+    # for the other ranks' parity checks, which run together
+    cpu['rank_threads'] = max(1, cpu['threads'] // local_world)
+    nthreads = min(16, cpu['rank_threads'])      # generator / host-prep threads (box CPU share)
 
     cfg = args.config
     n_per = args.files_per_gpu or DEFAULT_FILES[cfg]
@@ -404,7 +509,7 @@ def main():
     stream = torch.cuda.Stream()          # a real (non-null) stream: kernels and HIP events share it
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, distributed)
+    wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, group)
     total_files = n_per * world
     value = total_files * args.steps / wall
     traffic, traffic_src = traffic_for(cfg if cfg != '5-T600' else '5_T600', n_per, run.T,
@@ -413,29 +518,37 @@ def main():
 
     # ---- results: gathers (outside the timed region) -------------------------
     extras = {}
+    if distributed:
+        extras['process_group'] = {'backend': group.backend, 'world_size': dist.get_world_size(),
+                                   'devices_visible': n_dev, 'ranks_per_device': -(-local_world // max(n_dev, 1))}
+    best = ov = score = None
     if not matrix_mode:
         t_g = time.perf_counter()
         best, ov, score = batch.download_match(sptr)
         host_gather_s = time.perf_counter() - t_g
         extras['host_gather_ms'] = host_gather_s * 1e3
-        extras['matches'] = int((best >= 0).sum())
+        extras['matches'] = int(group.reduce([int((best >= 0).sum())], 'sum')[0])
         if distributed:
-            # RCCL alternative: all_gather the 16-B/file results over xGMI (zero-copy views of the
-            # library's result buffers, packed on the device: licensee_amd/shard.py)
-            from licensee_amd.shard import device_results_packed
-            res = device_results_packed(batch)
-            out = torch.empty((world * n_per, 4), dtype=torch.int32, device='cuda')
-            torch.cuda.synchronize()
-            dist.barrier()
-            t_g = time.perf_counter()
-            dist.all_gather_into_tensor(out, res)
-            torch.cuda.synchronize()
-            rccl_s = time.perf_counter() - t_g
-            t = torch.tensor([host_gather_s, rccl_s], dtype=torch.float64, device='cuda')
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            extras['host_gather_ms'] = float(t[0]) * 1e3
-            extras['rccl_allgather_ms'] = float(t[1]) * 1e3
-            extras['gather_winner'] = 'host' if t[0] <= t[1] else 'rccl'
+            host_gather_s = group.reduce([host_gather_s], 'max')[0]
+            extras['host_gather_ms'] = host_gather_s * 1e3
+            if group.backend == 'nccl':
+                # RCCL alternative: all_gather the 16-B/file results over xGMI (zero-copy views of
+                # the library's result buffers, packed on the device: licensee_amd/shard.py)
+                from licensee_amd.shard import device_results_packed
+                res = device_results_packed(batch)
+                out = torch.empty((world * n_per, 4), dtype=torch.int32, device='cuda')
+                torch.cuda.synchronize()
+                dist.barrier()
+                t_g = time.perf_counter()
+                dist.all_gather_into_tensor(out, res)
+                torch.cuda.synchronize()
+                rccl_s = group.reduce([time.perf_counter() - t_g], 'max')[0]
+                del out
+                extras['rccl_allgather_ms'] = rccl_s * 1e3
+                extras['gather_winner'] = 'host' if host_gather_s <= rccl_s else 'rccl'
+            else:
+                extras['gather_winner'] = 'host'
+                extras['gather_note'] = 'ranks share a device: no RCCL communicator, host gather only'
 
     # ---- separately reported rates (never `value`): PCIe-inclusive end-to-end, host prep ----
     if rank == 0 and not matrix_mode and not args.probe and not args.no_extras:
@@ -518,58 +631,70 @@ def main():
 
     cpu_baseline = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         from oracle.native import bits_to_csr
         orc = oracle_for(corpus)
-        cpu_threads = cpu['threads']
-        # calibrate on a small slice, then size the sample to ~cpu_seconds of CPU work
-        cal = min(n_per, 4000)
-        csr = bits_to_csr(files.bits[:cal], corpus.n_vocab)
-        tc = time.perf_counter()
-        orc.match(files.bits[:cal], files.wordset_size[:cal], files.length[:cal], files.cc_false_positive[:cal],
-                  args.threshold, nthreads=1, mode=0, csr=csr)
-        per_file = (time.perf_counter() - tc) / cal
-        sample = int(min(n_per, max(cal, args.cpu_seconds / max(per_file, 1e-9))))
+        # rank 0 calibrates on a small slice and sizes the sample to ~cpu_seconds of CPU work;
+        # every rank then checks that many files of its own shard
+        sample = 0
+        if rank == 0:
+            cal = min(n_per, 4000)
+            csr = bits_to_csr(files.bits[:cal], corpus.n_vocab)
+            tc = time.perf_counter()
+            orc.match(files.bits[:cal], files.wordset_size[:cal], files.length[:cal], files.cc_false_positive[:cal],
+                      args.threshold, nthreads=1, mode=0, csr=csr)
+            per_file = (time.perf_counter() - tc) / cal
+            sample = int(min(n_per, max(cal, args.cpu_seconds / max(per_file, 1e-9))))
+        sample = group.bcast(sample)
         sl = slice(0, sample)
-        csr = bits_to_csr(files.bits[sl], corpus.n_vocab)
-        tc = time.perf_counter()
-        cb, co, cs = orc.match(files.bits[sl], files.wordset_size[sl], files.length[sl],
-                               files.cc_false_positive[sl], args.threshold, nthreads=cpu_threads, mode=0, csr=csr)
-        cpu_s = time.perf_counter() - tc
-        tc = time.perf_counter()
-        orc.match(files.bits[sl], files.wordset_size[sl], files.length[sl], files.cc_false_positive[sl],
-                  args.threshold, nthreads=cpu_threads, mode=1)
-        cpu_bits_s = time.perf_counter() - tc
-        cpu_baseline = {'value': sample / cpu_s, 'unit': 'files/s', 'cores': cpu_threads, 'kind': 'port',
-                        'sample': f'first {sample} files of the same synthetic workload, hash-set Set#& '
-                                  f'restatement (oracle/dice_ref.c), {cpu_threads} threads',
-                        'bitset_variant_files_per_s': sample / cpu_bits_s,
-                        'nproc': cpu['nproc'], 'affinity_cpus': cpu['affinity_cpus'],
-                        'cgroup_cpu_quota': cpu['cgroup_cpu_quota'], 'cpu_model': cpu['cpu_model']}
-        if not matrix_mode:
-            mism = int(np.sum(best[sl] != cb) + np.sum(ov[sl] != co) + np.sum(score[sl] != cs))
-            parity = {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
-        else:
-            parity = parity_sample(run, orc, sptr, cpu_threads, sample)
-            parity.pop('oracle_files_per_s', None)
+        baseline = {}
+
+        def check():
+            threads = cpu['threads'] if rank == 0 else cpu['rank_threads']
+            csr = bits_to_csr(files.bits[sl], corpus.n_vocab)
+            tc = time.perf_counter()
+            cb, co, cs = orc.match(files.bits[sl], files.wordset_size[sl], files.length[sl],
+                                   files.cc_false_positive[sl], args.threshold, nthreads=threads, mode=0, csr=csr)
+            baseline['hash_s'] = time.perf_counter() - tc
+            if rank == 0:
+                tc = time.perf_counter()
+                orc.match(files.bits[sl], files.wordset_size[sl], files.length[sl], files.cc_false_positive[sl],
+                          args.threshold, nthreads=threads, mode=1)
+                baseline['bits_s'] = time.perf_counter() - tc
+            if not matrix_mode:
+                mism = int(np.sum(best[sl] != cb) + np.sum(ov[sl] != co) + np.sum(score[sl] != cs))
+                return {'checked_files': sample, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)'}
+            res = parity_sample(run, orc, sptr, threads, sample)
+            res.pop('oracle_files_per_s', None)
+            return res
+
+        parity = staged_parity(group, check)
+        if rank == 0:
+            cpu_baseline = {'value': sample / baseline['hash_s'], 'unit': 'files/s', 'cores': cpu['threads'],
+                            'kind': 'port',
+                            'sample': f"first {sample} files of rank 0's shard of the same synthetic workload, "
+                                      f"hash-set Set#& restatement (oracle/dice_ref.c), {cpu['threads']} threads",
+                            'bitset_variant_files_per_s': sample / baseline['bits_s'],
+                            'nproc': cpu['nproc'], 'affinity_cpus': cpu['affinity_cpus'],
+                            'cgroup_cpu_quota': cpu['cgroup_cpu_quota'], 'cpu_model': cpu['cpu_model']}
 
     head = {'templates': run.T, 'vocab': run.V, 'kernel': KERNELS[run.match_kernel], 'program_entries': run.entries,
             'algorithmic_bytes_per_file': run.algo_bytes_per_file}
-    # ---- the other BASELINE configs, same run (N = 1) ---------------------------------------
-    if rank == 0 and world == 1 and not args.probe and args.extra_configs:
+    # ---- the other BASELINE configs, same run (every rank, its own shard) ------------------
+    if not args.probe and args.extra_configs:
         run.close()
         run = None
         extras['configs'] = {}
         for c in [int(x) if x.strip().isdigit() else x.strip() for x in args.extra_configs.split(',') if x.strip()]:
             if c == cfg:
                 continue
-            r = Run(c, DEFAULT_FILES[c], 0, 1, dev, nthreads, args)
+            r = Run(c, args.extra_files_per_gpu or DEFAULT_FILES[c], rank, world, dev, nthreads, args)
             variants = [(str(c), None)]
             if c == 3 and r.match_kernel == 4:
                 variants.append(('3-allpairs', {'DICE_POST_PRUNE': '0'}))
             for tag, env in variants:
                 saved = r.rescore(env, dev) if env else None
-                extras['configs'][tag] = measure_extra(r, c, args, stream, sptr, cpu)
+                extras['configs'][tag] = measure_extra(r, c, args, stream, sptr, cpu, group)
                 if saved:
                     r.restore(saved)
             r.close()
@@ -591,7 +716,10 @@ def main():
                          'traffic_source': traffic_src,
                          'algorithmic_bytes_per_file': head['algorithmic_bytes_per_file'], 'launch_ms': launch_ms,
                          **({'note': 'config 3 is latency/issue-bound, not HBM-bound; frac is its HBM share '
-                                     'only (DESIGN.md 4b)'} if cfg == 3 else {})},
+                                     'only (DESIGN.md 4b)'} if cfg == 3 else {}),
+                         **({'per_rank_note': 'achieved = one rank\'s bytes / the slowest rank\'s launch time '
+                                              '(per-GPU roofline; every rank runs the same shard size)'}
+                            if world > 1 else {})},
             'cpu_baseline': cpu_baseline,
             'scores_per_s': value * head['templates'],
             'parity': parity,
@@ -602,6 +730,7 @@ def main():
     if run is not None:
         run.close()
     if distributed:
+        group.barrier()
         dist.destroy_process_group()
 
 

@@ -52,6 +52,34 @@ class _Files(ctypes.Structure):
 _lib = None
 
 
+def hip_runtime_path() -> Optional[str]:
+    """The HIP runtime this process should share: LICENSEE_DICE_HIP_RUNTIME if set ('' = none),
+    else the copy torch ships (torch/lib/libamdhip64.so, soname libamdhip64.so.7) when torch is
+    installed -- found without importing torch."""
+    env = os.environ.get('LICENSEE_DICE_HIP_RUNTIME')
+    if env is not None:
+        return env or None
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec('torch')
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.origin:
+        return None
+    p = os.path.join(os.path.dirname(spec.origin), 'lib', 'libamdhip64.so')
+    return p if os.path.exists(p) else None
+
+
+def _preload_hip_runtime():
+    """One HIP runtime per process. liblicensee_dice.so needs libamdhip64.so.7 by soname; if the
+    runtime torch uses is mapped first, the library binds to it, and torch (imported before or
+    after) keeps one runtime and one device view. Loaded the other way round, /opt/rocm's copy
+    and torch's would both be mapped, and dice_create refuses that (dice_last_error names both)."""
+    p = hip_runtime_path()
+    if p:
+        ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+
+
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load liblicensee_dice.so (raises if it was not built -- no fallback). LICENSEE_DICE_LIB
     names another build of the same library (A/B of compile-time kernel variants)."""
@@ -61,6 +89,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise DiceError(f'{path} is missing: build it with `python -c "import __graft_entry__ as g; g.build()"`')
+    _preload_hip_runtime()
     lib = ctypes.CDLL(path)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {
@@ -262,6 +291,7 @@ class DeviceBatch:
         b = ctypes.c_void_p()
         _check(load_library().dice_batch_create(scorer._ctx, int(capacity), ctypes.byref(b)))
         self._b = b
+        self.capacity = int(capacity)
         self.n = 0
 
     def close(self):

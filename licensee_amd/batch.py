@@ -44,8 +44,22 @@ class BatchDetector:
         self.host = HostPrep(self.engine.corpus)
         self.nthreads = nthreads
         self.exact_on = exact_on if self.host.field_need is not None else 'host'
+        self._batch = None          # one device batch, reused by every detect() and grown on demand
         if self.exact_on == 'device':
             self.engine.scorer.exact_setup(*exact_tables(self.engine.corpus, self.host))
+
+    def _device_batch(self, n: int):
+        if self._batch is None or self._batch.capacity < n:
+            if self._batch is not None:
+                self._batch.close()
+            cap = max(n, 64) if self._batch is None else max(n, 2 * self._batch.capacity)
+            self._batch = self.engine.scorer.batch(cap)
+        return self._batch
+
+    def close(self):
+        if self._batch is not None:
+            self._batch.close()
+            self._batch = None
 
     def detect(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
                threshold=None) -> List[Detection]:
@@ -53,15 +67,12 @@ class BatchDetector:
         if self.exact_on == 'device':
             fb, copyright, fmask, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads,
                                                            field_masks=True)
-            b = self.engine.scorer.batch(max(fb.n, 1))
-            try:
-                b.upload(fb)
-                b.exact(fmask)
-                b.match(float(thr))
-                exact = b.download_exact()
-                best, _, score = b.download_match()
-            finally:
-                b.close()
+            b = self._device_batch(max(fb.n, 1))
+            b.upload(fb)
+            b.exact(fmask)
+            b.match(float(thr))
+            exact = b.download_exact()
+            best, _, score = b.download_match()
         else:
             fb, copyright, exact, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads)
             best, _, score = self.engine.scorer.match(fb, float(thr))

@@ -12,6 +12,10 @@
 //   results : best (i32), overlap (u32), score (f64) per file, SoA.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <link.h>
+#include <sys/stat.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -315,9 +319,8 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
-    void* plan[] = {c->d_lrec, c->d_lep, c->d_les, c->d_lwt, c->d_pwrow, c->d_prow, c->d_povf, c->d_pdm, c->d_ptc,
-                    c->d_q8, c->d_qoff, c->d_qrec, c->d_qtc, c->d_q3tc, c->d_q3cc, c->d_p4q8, c->d_p4tc,
-                    c->d_p4cc, c->d_p4off, c->d_p4rec, c->d_p4slot, c->d_p4orig};
+    void* plan[] = {c->d_lrec, c->d_lep,  c->d_les,  c->d_lwt,   c->d_pwrow, c->d_prow,  c->d_povf, c->d_pdm,
+                    c->d_ptc,  c->d_p4q8, c->d_p4tc, c->d_p4cc,  c->d_p4off, c->d_p4rec, c->d_p4slot};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -330,14 +333,58 @@ static void ctx_free(dice_ctx* c) {
     delete c;
 }
 
+// One HIP runtime per process. The library binds libamdhip64.so.7 by soname, so it shares the
+// runtime of a host that loaded one first (torch ships its own copy under that soname). A host
+// that maps a second copy after this library -- a different file, so a second HSA runtime with
+// its own view of the devices -- can find no GPU. Refuse to create a context once two distinct
+// runtime files are mapped, naming both, instead of failing later in the other runtime.
+static int check_hip_runtime(std::string* ours) {
+    Dl_info di;
+    if (dladdr(reinterpret_cast<void*>(&hipGetDeviceCount), &di) && di.dli_fname) *ours = di.dli_fname;
+    struct Seen {
+        std::vector<std::pair<dev_t, ino_t>> ids;
+        std::vector<std::string> paths;
+    } seen;
+    dl_iterate_phdr(
+        [](dl_phdr_info* info, size_t, void* p) -> int {
+            auto* s = static_cast<Seen*>(p);
+            const char* name = info->dlpi_name;
+            const char* base = name ? std::strrchr(name, '/') : nullptr;
+            base = base ? base + 1 : name;
+            struct stat st;
+            if (!base || std::strncmp(base, "libamdhip64.so", 14) != 0 || stat(name, &st) != 0) return 0;
+            for (auto& id : s->ids)
+                if (id.first == st.st_dev && id.second == st.st_ino) return 0;
+            s->ids.emplace_back(st.st_dev, st.st_ino);
+            s->paths.emplace_back(name);
+            return 0;
+        },
+        &seen);
+    if (seen.paths.size() > 1) {
+        std::string msg = "two HIP runtimes are mapped in this process (";
+        for (size_t i = 0; i < seen.paths.size(); ++i) msg += (i ? ", " : "") + seen.paths[i];
+        msg += "); liblicensee_dice.so uses " + *ours +
+               ": load the host's HIP runtime (e.g. torch's) before liblicensee_dice.so";
+        return fail(DICE_E_DEVICE, msg);
+    }
+    return DICE_OK;
+}
+
 int dice_create(const dice_templates* t, int32_t device, dice_ctx** out) {
     if (!out) return fail(DICE_E_ARG, "out is NULL");
     *out = nullptr;
     if (!t || t->n_templates < 1 || t->n_vocab < 1 || !t->lf_bits || !t->lf_size ||
         !t->fields_set_size || !t->length_slack || !t->length || !t->is_cc)
         return fail(DICE_E_ARG, "invalid dice_templates");
+    std::string runtime = "libamdhip64";
+    if (int rc = check_hip_runtime(&runtime)) return rc;
     int ndev = 0;
-    HIP_TRY(hipGetDeviceCount(&ndev));
+    const hipError_t ec = hipGetDeviceCount(&ndev);
+    if (ec != hipSuccess || ndev < 1) {
+        (void)hipGetLastError();
+        return fail(DICE_E_DEVICE, "the HIP runtime " + runtime + " reports no device" +
+                                       (ec != hipSuccess ? std::string(" (") + hipGetErrorString(ec) + ")" : ""));
+    }
     if (device < 0 || device >= ndev) return fail(DICE_E_DEVICE, "device ordinal out of range");
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));

@@ -59,6 +59,9 @@ int run_shards(dice_ctx* const* ctxs, int32_t n_ctx, int64_t n, F&& fn) {
         sh[i].hi = n * (i + 1) / n_ctx;
     }
     auto body = [&](int32_t i) {
+        // the shard's launch checks read HIP's per-thread last error: start from a clean one
+        // (shard 0 runs on the caller's thread, which may hold a stale error of its own)
+        (void)hipGetLastError();
         if (hipSetDevice(ctxs[i]->device) != hipSuccess) {
             sh[i].rc = DICE_E_DEVICE;
             sh[i].err = "hipSetDevice failed";
@@ -100,11 +103,21 @@ constexpr size_t kStageBytes = (size_t)32 << 20;   // per staging buffer (two pe
 int upload_shard(dice_ctx* c, dice_batch* b, const dice_files* part) {
     const size_t row = (size_t)c->w64 * 8, bytes = (size_t)part->n_files * row;
     if (bytes < 2 * kStageBytes || is_pinned(part->bits)) return dice_batch_upload(b, part, nullptr);
-    if (!c->h_stage[0]) {
-        for (int i = 0; i < 2; ++i) {
-            if (hipHostMalloc(&c->h_stage[i], kStageBytes, hipHostMallocDefault) != hipSuccess ||
-                hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming) != hipSuccess)
-                return fail(DICE_E_NOMEM, "pinned staging allocation failed");
+    if (!c->h_stage_bytes) {
+        // all four resources or none: a partial set is freed, so the next call retries cleanly
+        bool ok = true;
+        for (int i = 0; i < 2 && ok; ++i)
+            ok = (c->h_stage[i] || hipHostMalloc(&c->h_stage[i], kStageBytes, hipHostMallocDefault) == hipSuccess) &&
+                 (c->stage_ev[i] || hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming) == hipSuccess);
+        if (!ok) {
+            (void)hipGetLastError();
+            for (int i = 0; i < 2; ++i) {
+                if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
+                if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
+                c->h_stage[i] = nullptr;
+                c->stage_ev[i] = nullptr;
+            }
+            return fail(DICE_E_NOMEM, "pinned staging allocation failed");
         }
         c->h_stage_bytes = kStageBytes;
     }
@@ -139,7 +152,9 @@ bool enable_peer(dice_ctx* from, int to) {
     if (ok) {
         const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
         ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
-        if (!ok) (void)hipGetLastError();
+        // any non-success return (AlreadyEnabled included) leaves HIP's per-thread last error
+        // set; the shard launch checks on this thread would read it as their own failure
+        if (e != hipSuccess) (void)hipGetLastError();
     }
     if (prev >= 0) (void)hipSetDevice(prev);
     if (ok) from->peer_mask |= 1ull << to;

@@ -15,10 +15,10 @@ def pytest_configure(config):
 
 
 def pytest_sessionstart(session):
-    """GPU sessions: let torch's HIP runtime initialize before liblicensee_dice.so loads, as bench.py
-    does. Both resolve the same libamdhip64 soname; when the library (built against /opt/rocm)
-    loads it first, torch's later device query can find no GPU, and the tests that use torch for
-    streams, graphs or pinned memory would fail depending on test order."""
+    """GPU sessions: initialize torch's HIP runtime up front. The library shares it either way
+    (licensee_amd._native maps torch's runtime before liblicensee_dice.so; tests/test_runtime.py
+    checks the library-first order), so this only moves torch's device start-up out of the first
+    test's time limit."""
     markexpr = getattr(session.config.option, 'markexpr', '') or ''
     if 'gpu' in markexpr and 'not gpu' not in markexpr:
         try:

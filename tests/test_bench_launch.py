@@ -1,0 +1,63 @@
+"""bench.py --gpus N starts its own ranks: with no RANK in the environment
+the parent makes no GPU call, runs a child torch.distributed.run on 127.0.0.1 and relays rank 0's
+JSON line. CPU: the launcher with a stub rank script (gloo, world size 2). GPU: the real bench at
+--gpus 2 on the one-GPU box (both ranks on device 0, gloo coordination): n_gpus 2, a cpu_baseline
+and zero parity mismatches summed over both ranks' shards."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+STUB = '''
+import json, os, sys
+import torch.distributed as dist
+dist.init_process_group('gloo')
+import torch
+t = torch.tensor([float(dist.get_rank() + 1)])
+dist.all_reduce(t)
+if dist.get_rank() == 0:
+    print('banner line a native library might print')
+    print(json.dumps({'world': dist.get_world_size(), 'sum': float(t[0]), 'argv': sys.argv[1:]}))
+dist.destroy_process_group()
+'''
+
+
+def test_self_launch_relays_rank0_line(tmp_path):
+    stub = tmp_path / 'rank.py'
+    stub.write_text(STUB)
+    code = ('import sys; sys.path.insert(0, %r); import bench; '
+            'sys.exit(bench.self_launch(2, ["--steps", "3"], script=%r))' % (ROOT, str(stub)))
+    p = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = p.stdout.strip().splitlines()
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out == {'world': 2, 'sum': 3.0, 'argv': ['--steps', '3']}
+
+
+def test_external_launch_must_match_gpus():
+    env = dict(os.environ, RANK='0', WORLD_SIZE='2', LOCAL_RANK='0', MASTER_PORT='1', MASTER_ADDR='127.0.0.1')
+    p = subprocess.run([sys.executable, 'bench.py', '--gpus', '4'], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=env)
+    assert p.returncode != 0 and 'WORLD_SIZE=2 but --gpus 4' in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu():
+    cmd = [sys.executable, 'bench.py', '--gpus', '2', '--steps', '3', '--warmup', '1', '--files-per-gpu', '40000',
+           '--extra-configs', '3,5', '--extra-files-per-gpu', '20000', '--no-extras', '--cpu-seconds', '1']
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line['n_gpus'] == 2 and line['config']['global_files'] == 80000
+    assert line['extras']['process_group']['world_size'] == 2
+    assert line['cpu_baseline'] and line['cpu_baseline']['value'] > 0
+    assert line['parity']['mismatches'] == 0 and line['parity']['ranks_checked'] == 2
+    for tag in ('3', '3-allpairs', '5'):
+        rec = line['extras']['configs'][tag]
+        assert rec['global_files'] == 40000 and rec['parity']['mismatches'] == 0, (tag, rec)
+        assert rec['cpu_baseline']['value'] > 0

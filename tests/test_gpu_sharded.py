@@ -60,6 +60,25 @@ def test_match_sharded_equals_single(vendored, gather):
 
 
 @pytest.mark.parametrize('gather', [0, 1])
+def test_stale_hip_error_on_caller_thread_is_not_a_shard_failure(vendored, gather):
+    """ADVICE r3 (dice_shard.cpp enable_peer): a non-success HIP return leaves the calling thread's
+    last error set; shard 0 runs on that thread and its launch checks read hipGetLastError. A stale
+    error (as hipDeviceEnablePeerAccess -> AlreadyEnabled leaves) must not fail the call."""
+    import ctypes
+
+    from licensee_amd._native import hip_runtime_path, match_sharded
+    corpus, fb, scs = vendored
+    hip = ctypes.CDLL(hip_runtime_path() or 'libamdhip64.so.7')
+    part = _sub(fb, 4097)
+    ref = scs[0].match(part, 98.0)
+    assert hip.hipSetDevice(ctypes.c_int(1 << 20)) != 0      # invalid ordinal: sets the sticky error
+    got = match_sharded(scs[:2], part, 98.0, gather)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    assert hip.hipGetLastError() == 0
+
+
+@pytest.mark.parametrize('gather', [0, 1])
 def test_matrix_sharded_equals_single(vendored, gather):
     from licensee_amd._native import matrix_sharded
     corpus, fb, scs = vendored
