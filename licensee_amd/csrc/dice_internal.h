@@ -83,21 +83,14 @@ struct dice_ctx {
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0, post_ld = 0;
     bool post_fast = false;
     int64_t post_rows = 0;
-    // kind 3 match mode, bound-pruned (dice_prune.hip): per-template group counts, records
-    void* d_q8 = nullptr;      // [padded T] uint4: |Lf ∩ group g| clamped to bytes
-    void* d_qoff = nullptr;    // [T + 1] u32 record offsets
-    void* d_qrec = nullptr;    // [records] uint4 {u64 word index, mask lo, mask hi, 0}
-    void* d_qtc = nullptr;     // [padded T] uint4 template constants (dice_prune.hip)
-    void* d_q3tc = nullptr;    // [704] uint4 v3 constants {length, -max(slack, 0), 4 base - 3, sum of group bytes}
-    void* d_q3cc = nullptr;    // [704] u32 v3 CC masks (~0: a cc-* template)
+    // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --
+    // group bytes, constants, CC masks, template index | record offset, records, slot bounds
     bool prune = false, prune_zero_base = false;
-    uint32_t prune_wf_noclamp = 0;   // v3: |W_F| from which the bound's length term needs no clamp
-    // v4 (dice_prune4): the v3 tables in position (length-sorted) order, slot bounds, position map
+    uint32_t prune_wf_noclamp = 0;   // |W_F| from which the bound's length term needs no clamp
     void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
-         *d_p4slot = nullptr, *d_p4orig = nullptr;
+         *d_p4slot = nullptr;
     int32_t p4_zkeep[2] = {-1, -1}, p4_zpos[2] = {0, 0};
-    int32_t prune_sched = 0, n_cu = 256, prune_diag = 0, prune_max_evals = 8, prune_route = 12;
-    int64_t prune_records = 0;
+    int32_t n_cu = 256, prune_max_evals = 8, prune_route = 16;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
     // two page-locked staging buffers for shard uploads from pageable caller memory
     uint64_t peer_mask = 0;

@@ -12,7 +12,7 @@ hash mode (the Set#& restatement of content_helper.rb:128-133) and against the p
     files, files outside the fast envelope (|W_F| >= 2^20, len_F >= 2^21);
   * exact ties: duplicated templates, where the later key must win (dice.rb:39);
   * a tiny vocabulary (one u64 word per lane) and T = 700 (11 templates per lane);
-  * every schedule variant (DICE_PRUNE_SCHED) and ragged batch sizes.
+  * the deferral knobs (exact scores before deferral, the routing point) and ragged batch sizes.
 """
 import numpy as np
 import pytest
@@ -32,13 +32,13 @@ def _oracle(c):
     return OracleScorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, c.n_vocab)
 
 
-def _match_all(c, fb, thresholds, monkeypatch, sched=None):
+def _match_all(c, fb, thresholds, monkeypatch, env=None):
     """Match results of the pruned kernel and of the postings kernel, per threshold."""
     out = {}
     for prune in ('1', '0'):
         monkeypatch.setenv('DICE_POST_PRUNE', prune)
-        if sched is not None:
-            monkeypatch.setenv('DICE_PRUNE_SCHED', str(sched))
+        for k, v in (env or {}).items():
+            monkeypatch.setenv(k, v)
         sc = _scorer(c)
         try:
             assert sc.info()[2] == 3
@@ -47,7 +47,8 @@ def _match_all(c, fb, thresholds, monkeypatch, sched=None):
         finally:
             sc.close()
     monkeypatch.delenv('DICE_POST_PRUNE', raising=False)
-    monkeypatch.delenv('DICE_PRUNE_SCHED', raising=False)
+    for k in (env or {}):
+        monkeypatch.delenv(k, raising=False)
     return out['1'], out['0']
 
 
@@ -59,8 +60,8 @@ def _assert_same(got, exp, where):
     assert np.array_equal(best, eb), (where, np.nonzero(best != eb)[0][:10])
 
 
-def _check(c, fb, monkeypatch, thresholds=(98.0, 0.0, 100.5), sched=None):
-    pruned, full = _match_all(c, fb, thresholds, monkeypatch, sched)
+def _check(c, fb, monkeypatch, thresholds=(98.0, 0.0, 100.5), env=None):
+    pruned, full = _match_all(c, fb, thresholds, monkeypatch, env)
     orc = _oracle(c)
     for thr in thresholds:
         exp = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, thr, nthreads=16, mode=0)
@@ -85,15 +86,19 @@ def test_config3_files(config3, monkeypatch):
     assert 0.3 < np.mean(best >= 0) < 0.9   # the workload matches some files, not all
 
 
-@pytest.mark.parametrize('sched', [0, 1, 2, 3, 4, 5])
+KNOBS = [{}, {'DICE_PRUNE_MAX_EVALS': '1'}, {'DICE_PRUNE_MAX_EVALS': '0'}, {'DICE_PRUNE_ROUTE': '0'},
+         {'DICE_PRUNE_ROUTE_AT': '1'}, {'DICE_PRUNE_ROUTE': '600', 'DICE_PRUNE_ROUTE_AT': '4'}]
+
+
+@pytest.mark.parametrize('knob', range(len(KNOBS)))
 @pytest.mark.parametrize('n', [1, 63, 64, 65, 129, 1000])
-def test_schedules_and_ragged_batches(config3, sched, n, monkeypatch):
+def test_deferral_knobs_and_ragged_batches(config3, knob, n, monkeypatch):
     from licensee_amd._native import FileBatch
     c, fb = config3
     lo = 517
     part = FileBatch(fb.bits[lo:lo + n], fb.wordset_size[lo:lo + n], fb.length[lo:lo + n],
                      fb.cc_false_positive[lo:lo + n])
-    _check(c, part, monkeypatch, thresholds=(98.0, 0.0), sched=sched)
+    _check(c, part, monkeypatch, thresholds=(98.0, 0.0), env=KNOBS[knob])
 
 
 def _random_files(c, n, seed, density):

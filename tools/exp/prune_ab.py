@@ -3,7 +3,7 @@
     python tools/exp/prune_ab.py [--n N] [--reps R] [--profiles 0,1] VARIANT ...
 
 VARIANT is name or name:ENV=VAL,ENV=VAL (environment read at dice_create), e.g.
-    v3  old:DICE_PRUNE_SCHED=1  post:DICE_POST_PRUNE=0  route6:DICE_PRUNE_ROUTE=6
+    base  post:DICE_POST_PRUNE=0  route6:DICE_PRUNE_ROUTE=6
 Workload: the bench's config-3 corpus (600 synthetic templates); profile 0 = config-3 files,
 profile 1 = long/mixed files (concatenations of 2-6 templates plus notices). Every variant's
 results are checked equal to the first variant's; prints ms per launch (median of the reps,
