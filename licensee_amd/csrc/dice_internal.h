@@ -80,7 +80,7 @@ struct dice_ctx {
     void* d_povf = nullptr;    // flat u16 template ids of the long words
     void* d_pdm = nullptr;     // [T][16] u64 dense-prefix masks
     void* d_ptc = nullptr;     // [T] int4 template constants
-    int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_diag = 0, post_ld = 0;
+    int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_ld = 0;
     bool post_fast = false;
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --

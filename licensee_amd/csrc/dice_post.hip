@@ -46,8 +46,10 @@ namespace dice {
 #ifndef DENSE_TU
 #define DENSE_TU 2
 #endif
-#ifndef POST_PREFETCH_WORDS
-#define POST_PREFETCH_WORDS 0   // 1: prefetch_file also loads the first word chunks (spills at 64 VGPRs)
+// Phase-skip diagnostics (tools/build_variant.sh -DPOST_DIAG=n; results are wrong): 1 skips the
+// dense kernel, 2 the postings walk, 4 the narrow-word extraction, 8 scoring
+#ifndef POST_DIAG
+#define POST_DIAG 0
 #endif
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
@@ -224,63 +226,104 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     }
 }
 
-// Phase 2 for one file: queue its narrow words (set bits of u64 words >= pb0) and walk their
-// postings into the wave's counter row.
-template <int WCAP>
-__device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
-                                              const uint64_t (&first)[kChunks], uint32_t* wq, uint2* lq,
-                                              const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-                                              uint32_t* crow32, int lane, int32_t diag) {
-    uint32_t nq = 0;           // queued narrow words (wave-uniform)
-    uint32_t nl = 0;           // queued long words (uniform)
+// The file's dense partials into its counter row (a plain copy, u16 pairs widened: this wave's
+// postings adds for the file come after it; the copy writes every entry, so the row is never
+// re-zeroed), one LDS address and immediate offsets.
+template <int PJ>
+__device__ __forceinline__ void copy_in(uint32_t* crow32, const uint32_t (&part)[PJ], int32_t tp, int lane) {
+    uint2* dst = reinterpret_cast<uint2*>(crow32) + lane;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j)
+        if (lane + j * kWave < tp / 2) dst[j * kWave] = make_uint2(part[j] & 0xFFFFu, part[j] >> 16);
+}
 
-    // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
-    // together. Per chunk a wave prefix sum of the lanes' bit counts gives every lane its
-    // queue slots, and each lane writes its own words (a chunk of more than WCAP words
-    // -- a file holding most of the vocabulary -- goes round by round instead).
-    for (int32_t pb = pb0; pb < w64; pb += kChunks * kWave) {
-        uint64_t xs[kChunks];
+__device__ __forceinline__ void load_chunks(const uint64_t* __restrict__ row, int32_t w64, int32_t pb, int lane,
+                                            uint64_t (&xs)[kChunks]) {
 #pragma unroll
-        for (int c = 0; c < kChunks; ++c) {
-            const int32_t p = pb + c * kWave + lane;
-            xs[c] = (POST_PREFETCH_WORDS && pb == pb0) ? first[c] : (p < w64 ? row[p] : 0);
+    for (int c = 0; c < kChunks; ++c) {
+        const int32_t p = pb + c * kWave + lane;
+        xs[c] = p < w64 ? row[p] : 0;
+    }
+}
+
+// One round of kChunks x 64 file words: per chunk a wave prefix sum of the lanes' bit counts
+// gives every lane its queue slots, and each lane writes its own words (a chunk of more than
+// WCAP words -- a file holding most of the vocabulary -- goes round by round instead); a full
+// queue is walked.
+template <int WCAP>
+__device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int32_t pb, uint32_t* wq, uint32_t& nq,
+                                             uint2* lq, uint32_t& nl, const uint16_t* __restrict__ prow,
+                                             const uint16_t* __restrict__ plong, uint32_t* crow32, int lane) {
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+        const uint32_t wbase = (uint32_t)(pb + c * kWave + lane) * 64u;
+        uint64_t x = xs[c];
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(x);
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
+        if (total == 0) continue;
+        if (nq + total > WCAP) {
+            if (!(POST_DIAG & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
+            nq = 0;
         }
-#pragma unroll
-        for (int c = 0; c < kChunks; ++c) {
-            const uint32_t wbase = (uint32_t)(pb + c * kWave + lane) * 64u;
-            uint64_t x = xs[c];
-            const uint32_t cnt = (uint32_t)__builtin_popcountll(x);
-            const uint32_t incl = wave_incl_scan(cnt);
-            const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
-            if (total == 0) continue;
-            if (nq + total > WCAP) {
-                if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
-                nq = 0;
-            }
-            if (total <= WCAP) {
-                uint32_t pos = nq + incl - cnt;
-                while (x) {
-                    wq[pos++] = wbase + (uint32_t)__builtin_ctzll(x);
-                    x &= x - 1;
-                }
-                nq += total;
-                continue;
-            }
-            while (__any(x != 0)) {
-                const bool has = x != 0;
-                const uint32_t w = wbase + (has ? (uint32_t)__builtin_ctzll(x) : 0u);
+        if (total <= WCAP) {
+            uint32_t pos = nq + incl - cnt;
+            while (x) {
+                wq[pos++] = wbase + (uint32_t)__builtin_ctzll(x);
                 x &= x - 1;
-                const uint64_t bal = __ballot(has);
-                if (has) wq[nq + lane_rank(bal)] = w;
-                nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
-                if (nq > WCAP - kWave) {
-                    if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
-                    nq = 0;
-                }
+            }
+            nq += total;
+            continue;
+        }
+        while (__any(x != 0)) {
+            const bool has = x != 0;
+            const uint32_t w = wbase + (has ? (uint32_t)__builtin_ctzll(x) : 0u);
+            x &= x - 1;
+            const uint64_t bal = __ballot(has);
+            if (has) wq[nq + lane_rank(bal)] = w;
+            nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
+            if (nq > WCAP - kWave) {
+                if (!(POST_DIAG & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
+                nq = 0;
             }
         }
     }
-    if (!(diag & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
+}
+
+// Phase 2 for one file: queue its narrow words (set bits of u64 words >= pb0) and walk their
+// postings into the wave's counter row. LATE (matrix mode): the file's dense partials are loaded
+// here, before its first word chunks, and copied in once those are requested -- instead of being
+// prefetched into registers during the previous file's scoring, where the matrix kernel cannot
+// afford them.
+template <int WCAP, bool LATE, int PJ>
+__device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
+                                              const uint32_t* __restrict__ psrc, int32_t tp, uint32_t* wq, uint2* lq,
+                                              const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+                                              uint32_t* crow32, int lane) {
+    uint32_t nq = 0;           // queued narrow words (wave-uniform)
+    uint32_t nl = 0;           // queued long words (uniform)
+    // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
+    // together (queue_chunks). The first round is peeled so that LATE's partials are copied in
+    // between its loads and their use and are dead for the rest of the file.
+    int32_t pb = pb0;
+    uint64_t xs[kChunks];
+    if (LATE) {
+        uint32_t part[PJ];
+        // unconditional loads at clamped indices: copy_in masks the pairs past tp / 2
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) part[j] = psrc[min(lane + j * kWave, tp / 2 - 1)];
+        if (pb < w64) load_chunks(row, w64, pb, lane, xs);
+        copy_in<PJ>(crow32, part, tp, lane);
+        if (pb < w64) {
+            queue_chunks<WCAP>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
+            pb += kChunks * kWave;
+        }
+    }
+    for (; pb < w64; pb += kChunks * kWave) {
+        load_chunks(row, w64, pb, lane, xs);
+        queue_chunks<WCAP>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
+    }
+    if (!(POST_DIAG & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
     walk_long(lq, nl, plong, crow32, lane);
 }
 
@@ -311,6 +354,20 @@ __device__ __forceinline__ void lane_best(const uint32_t* crow32, const uint2* t
 #ifndef POST_MATRIX_STORE
 #define POST_MATRIX_STORE 3
 #endif
+#define DICE_STR(x) #x
+#define DICE_UNROLL(n) _Pragma(DICE_STR(unroll n))
+#ifndef SCORE_UNROLL
+#define SCORE_UNROLL 10
+#endif
+// A pointer every lane holds the same value of, as SGPRs.
+template <class E>
+__device__ __forceinline__ E* uniform_ptr(E* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<E*>(lo | (hi << 32));
+}
+
 template <bool kMatrix, int TJ, bool FAST>
 __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs, int32_t T, int32_t ld, int64_t file, uint32_t wf,
                                              int32_t lf, bool cc, double thr, int32_t* __restrict__ best_out,
@@ -319,36 +376,41 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
                                              int32_t* __restrict__ tki, double* __restrict__ tks, int lane) {
     int32_t bi = -1, bd = 1;
     uint32_t bo = 0;
-    // the file's row bases (wave-uniform) and the lane's offset: every store of the unrolled loop
-    // is base + lane offset + an immediate (< 4 KiB: the score row restarts at template 320), so
-    // no per-template 64-bit address stays live (they spilled, and each scratch reload's
-    // vmcnt(0) waited for every store issued before it)
-    uint32_t* orow = kMatrix ? mov + file * ld : nullptr;
-    double* srow0 = kMatrix ? msc + file * ld : nullptr;
-    double* srow1 = srow0 + 5 * kWave;
-#pragma unroll
+    // The file's row bases as SGPR values (readfirstlane: the compiler cannot fold a lane offset
+    // into a hoisted per-lane 64-bit base) and the lane opaque per file: every store is SGPR base +
+    // a 32-bit VGPR offset formed where it is used, so no per-lane address stays live across the
+    // file loop (they spilled to scratch, and each reload's vmcnt(0) waited for every store
+    // issued before it).
+    uint32_t* orow = nullptr;
+    double* srow = nullptr;
+    uint32_t lo = (uint32_t)lane;
+    if (kMatrix) {
+        orow = uniform_ptr(mov + file * ld);
+        srow = uniform_ptr(msc + file * ld);
+        asm volatile("" : "+v"(lo));
+    }
+    DICE_UNROLL(SCORE_UNROLL)
     for (int j = 0; j < TJ; ++j) {
-        const int32_t t = lane + j * kWave;
+        const int32_t t = (int32_t)lo + j * kWave;
         if (t < T) {
             uint32_t ov;
             int32_t den;
             lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             if (kMatrix) {
 #if POST_MATRIX_STORE == 3
-                __builtin_nontemporal_store(ov, &orow[t]);
-                __builtin_nontemporal_store(dice_score(ov, den), j < 5 ? &srow0[t] : &srow1[t - 5 * kWave]);
+                __builtin_nontemporal_store(ov, orow + t);
+                __builtin_nontemporal_store(dice_score(ov, den), srow + t);
 #else
                 const double sc = dice_score(ov, den);
-                double* sp = j < 5 ? &srow0[t] : &srow1[t - 5 * kWave];
                 // diagnostics (POST_MATRIX_STORE, A/B builds only): bit 0 / 1 store overlaps / scores
                 // (a cleared bit still computes them), bit 2 plain stores instead of nontemporal
                 if ((POST_MATRIX_STORE & 1) || ov == 0xFFFFFFFFu) {
                     if (POST_MATRIX_STORE & 4) orow[t] = ov;
-                    else __builtin_nontemporal_store(ov, &orow[t]);
+                    else __builtin_nontemporal_store(ov, orow + t);
                 }
                 if ((POST_MATRIX_STORE & 2) || ov == 0xFFFFFFFFu) {
-                    if (POST_MATRIX_STORE & 4) *sp = sc;
-                    else __builtin_nontemporal_store(sc, sp);
+                    if (POST_MATRIX_STORE & 4) srow[t] = sc;
+                    else __builtin_nontemporal_store(sc, srow + t);
                 }
 #endif
             }
@@ -415,30 +477,19 @@ __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, i
 // A file's loads that do not depend on its walk -- dense partials, scalars, first word chunks --
 // issued while the wave is still scoring the previous file (prefetch_file), so they are in
 // flight during that file's scoring instead of heading this file's dependency chain.
-constexpr int kPJ = (kPostMaxTpad / 2 + kWave - 1) / kWave;   // u32 partial pairs per lane
+template <int TPMAX>
+constexpr int pairs_per_lane() { return (TPMAX / 2 + kWave - 1) / kWave; }   // u32 partial pairs per lane
 
-struct FilePre {
-    uint32_t part[kPJ];
-    uint64_t first[kChunks];
-};
-
-__device__ __forceinline__ void prefetch_file(int64_t pos, int64_t file, const uint64_t* __restrict__ rows, int32_t w64,
-                                              int32_t pb0, const uint16_t* __restrict__ dense, int32_t tp,
-                                              const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
-                                              const uint8_t* __restrict__ ccp, int lane, FilePre& p) {
+// A file's dense partials, loaded while the wave is still scoring the previous file (match
+// mode), so they are in flight during that file's scoring instead of heading this file's chain.
+template <int PJ>
+__device__ __forceinline__ void prefetch_partials(const uint16_t* __restrict__ dense, int64_t pos, int32_t tp,
+                                                  int lane, uint32_t (&part)[PJ]) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + pos * tp);
 #pragma unroll
-    for (int j = 0; j < kPJ; ++j) {
+    for (int j = 0; j < PJ; ++j) {
         const int32_t i = lane + j * kWave;
-        p.part[j] = i < tp / 2 ? src[i] : 0;
-    }
-    if (POST_PREFETCH_WORDS) {
-        const uint64_t* row = rows + file * w64;
-#pragma unroll
-        for (int c = 0; c < kChunks; ++c) {
-            const int32_t q = pb0 + c * kWave + lane;
-            p.first[c] = q < w64 ? row[q] : 0;
-        }
+        part[j] = i < tp / 2 ? src[i] : 0;
     }
 }
 
@@ -454,16 +505,16 @@ __device__ __forceinline__ void post_narrow_body(
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
+    int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
-    // diag (DICE_POST_DIAG, diagnostics only -- results are wrong): 2 skips the postings walk,
-    // 4 skips the narrow-word extraction, 8 skips scoring
     constexpr int kTJ = (TPMAX + kWave - 1) / kWave;           // templates per lane
     constexpr int kWCap = word_cap<TPMAX>();
+    constexpr int kPJ = pairs_per_lane<TPMAX>();
     __shared__ uint32_t cnt32[kPostWaves * TPMAX];             // u32 counters, one row per wave
     __shared__ uint2 tcs[TPMAX];                               // packed template constants
     __shared__ uint32_t wq[kPostWaves][kWCap];                 // queued narrow word ids
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
+    __shared__ uint2 tsc[kMatrix ? kPostWaves : 1][kPostFiles / kPostWaves];   // matrix: own files' {|W_F|, len_F}
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     uint32_t* crow32 = cnt32 + wave * TPMAX;
@@ -471,63 +522,66 @@ __device__ __forceinline__ void post_narrow_body(
     for (int i = lane; i < TPMAX; i += kWave) crow32[i] = 0;
     __syncthreads();
 
-    const int32_t pb0 = (diag & 4) ? w64 : D;
+    const int32_t pb0 = (POST_DIAG & 4) ? w64 : D;
     // indexed (idx != NULL, match mode): position i is the deferred file idx[i] of a pruned match
     // (its dense partials at i, its row, scalars and results at idx[i]); persistent tiles
     const int64_t nn = idx ? (int64_t)*pn : n;
     for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
+    if (kMatrix) asm volatile("" : "+s"(tp));   // (see Tf below)
     // the tile's file indices and scalars, lane l = tile file l, by vector loads; each file reads
     // them with v_readlane. (Scalar loads of the next file's |W_F| / len_F shared lgkmcnt with the
     // postings walk's LDS adds and reads, whose waits then stalled on HBM latency.)
-    const int64_t tpos = min(f0 + lane, nn - 1);
+    // files of this tile (uniform, 1..64): the tile's compares stay 32-bit scalar ones (64-bit
+    // signed compares go to the VALU and keep a VGPR copy of nn)
+    const int64_t rem64 = nn - f0;
+    const int32_t nt = (rem64 >> 32) != 0 || (uint32_t)rem64 >= (uint32_t)kPostFiles ? kPostFiles : (int32_t)rem64;
+    const int64_t tpos = f0 + min(lane, nt - 1);
+    // (indexed mode only: the file of tile position l; otherwise position = file, no register)
     const uint32_t tfile = idx ? (uint32_t)idx[tpos] : (uint32_t)tpos;
-    const uint32_t twf = wfp[tfile];
-    const uint32_t tlen = (uint32_t)lenp[tfile];
-    const uint32_t tcc = ccp[tfile];
-    FilePre pre;
-    if (f0 + wave < nn) {
-        const int64_t p0 = f0 + wave;
-        prefetch_file(p0, (int64_t)__builtin_amdgcn_readlane(tfile, wave), rows, w64, pb0, dense, tp, wfp, lenp, ccp,
-                      lane, pre);
+    uint32_t twf = wfp[tfile];
+    uint32_t tlen = (uint32_t)lenp[tfile];
+    const uint64_t tcc = __ballot(ccp[tfile] != 0);   // the tile's CC flags, one bit per file
+    if (kMatrix) {
+        // matrix mode: the wave's own files' |W_F| and len_F parked in its LDS slots instead of two
+        // VGPRs live across the whole tile (the scoring's registers need them)
+        uint32_t lw = (uint32_t)lane;
+        asm volatile("" : "+v"(lw));   // the slot address formed here, not hoisted out of the tile loop
+        if ((lw & (kPostWaves - 1)) == (uint32_t)wave) tsc[wave][lw >> 4] = make_uint2(twf, tlen);
     }
+    uint32_t pre[kPJ];   // match mode: the next file's dense partials (prefetched)
+    if (!kMatrix && wave < nt) prefetch_partials<kPJ>(dense, f0 + wave, tp, lane, pre);
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
         const int64_t pos = f0 + fi;
-        if (pos >= nn) break;   // wave-uniform
-        const int64_t file = (int64_t)rfl(__builtin_amdgcn_readlane(tfile, fi));
+        if (fi >= nt) break;   // wave-uniform
+        const int64_t file = idx ? (int64_t)rfl(__builtin_amdgcn_readlane(tfile, fi)) : pos;
         const uint64_t* row = rows + file * w64;
-        // this file's dense partials start its counter row (a plain copy, u16 pairs widened: the
-        // row is zero here and this wave's postings adds come after it)
-        if (!kMatrix) {
-            // one LDS address and immediate offsets: the match kernel then spills nothing (4 VGPRs
-            // before); the matrix kernel allocates better with per-j addresses
-            uint2* dst = reinterpret_cast<uint2*>(crow32) + lane;
-#pragma unroll
-            for (int j = 0; j < kPJ; ++j)
-                if (lane + j * kWave < tp / 2) dst[j * kWave] = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
+        // T, tp and ld opaque per file: the per-lane masks (t < T, i < tp / 2) and LDS addresses
+        // are then formed where they are used instead of being hoisted out of the file loop, where
+        // they stayed live as ~30 SGPRs and several VGPRs and spilled (the matrix kernel to scratch)
+        int32_t Tf = T, tpf = tp, ldf = ld;
+        int lanef = lane;   // likewise every lane-derived constant (lane + 64 j, lane addresses)
+        if (kMatrix) asm volatile("" : "+s"(Tf), "+s"(tpf), "+s"(ldf), "+v"(lanef));
+        // this file's dense partials start its counter row (matrix mode: inside file_postings)
+        if (!kMatrix) copy_in<kPJ>(crow32, pre, tpf, lanef);
+        uint32_t wf;
+        int32_t lf;
+        if (kMatrix) {
+            const uint2 sc = tsc[wave][fi >> 4];   // uniform address: a broadcast read
+            wf = rfl(sc.x);
+            lf = (int32_t)rfl(sc.y);
         } else {
-#pragma unroll
-            for (int j = 0; j < kPJ; ++j) {
-                const int32_t i = lane + j * kWave;
-                if (i < tp / 2) *reinterpret_cast<uint2*>(&crow32[2 * i]) = make_uint2(pre.part[j] & 0xFFFFu, pre.part[j] >> 16);
-            }
+            wf = rfl(__builtin_amdgcn_readlane(twf, fi));
+            lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
         }
-        const uint32_t wf = rfl(__builtin_amdgcn_readlane(twf, fi));
-        const int32_t lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
-        const bool cc = __builtin_amdgcn_readlane(tcc, fi) != 0;
-        uint64_t first[kChunks];
-#pragma unroll
-        for (int c = 0; c < kChunks; ++c) first[c] = POST_PREFETCH_WORDS ? pre.first[c] : 0;
-        file_postings<kWCap>(row, w64, pb0, first, wq[wave], lq[wave], prow, plong, crow32, lane, diag);
-        // the wave's next file: its independent loads fly while this one is scored
-        if (fi + kPostWaves < kPostFiles && pos + kPostWaves < nn) {
-            const int64_t pn1 = pos + kPostWaves;
-            prefetch_file(pn1, (int64_t)__builtin_amdgcn_readlane(tfile, fi + kPostWaves), rows, w64, pb0, dense, tp,
-                          wfp, lenp, ccp, lane, pre);
-        }
+        const bool cc = ((tcc >> fi) & 1u) != 0;
+        file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, reinterpret_cast<const uint32_t*>(dense + pos * tpf), tpf,
+                                           wq[wave], lq[wave], prow, plong, crow32, lanef);
+        // match mode: the wave's next file's partials fly while this one is scored
+        if (!kMatrix && fi + kPostWaves < nt) prefetch_partials<kPJ>(dense, pos + kPostWaves, tpf, lane, pre);
 
-        if (diag & 8) continue;
-        score_file<kMatrix, KM, kTJ>(crow32, tcs, T, ld, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
-                                            k, mov, msc, tki, tks, lane);
+        if (POST_DIAG & 8) continue;
+        score_file<kMatrix, KM, kTJ>(crow32, tcs, Tf, ldf, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
+                                            k, mov, msc, tki, tks, lanef);
     }
     }
 }
@@ -541,10 +595,10 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
+    int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
     post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn, ld);
+                               score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
 // POST_MATRIX_OCC (A/B): waves per SIMD the matrix kernel is compiled for (8: two workgroups
@@ -559,10 +613,10 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
-    int32_t* __restrict__ tki, double* __restrict__ tks, int32_t diag, bool corpus_fast,
+    int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
     post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
-                               score_out, k, mov, msc, tki, tks, diag, corpus_fast, idx, pn, ld);
+                               score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
 // ---- host side ---------------------------------------------------------------------------
@@ -666,8 +720,6 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
         hipMemcpy(c->d_ptc, tcv.data(), tcv.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "postings plan upload failed");
     c->post_dense = D;
-    const char* dg = diag_env("DICE_POST_DIAG");
-    c->post_diag = dg && *dg ? atoi(dg) : 0;
     c->post_tpad = tpad;
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
@@ -721,7 +773,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     const int64_t tiles = (b->n + kPostFiles - 1) / kPostFiles;
     // two workgroups per CU are resident in either kernel (LDS)
     const int64_t groups = idx ? std::min<int64_t>(tiles, 2 * (int64_t)c->n_cu) : tiles;
-    if (c->post_dense == 0 || (c->post_diag & 1)) {
+    if (c->post_dense == 0 || (POST_DIAG & 1)) {
         const int64_t rows = idx ? b->capacity : b->n;
         if (hipMemsetAsync(b->d_pdense, 0, (size_t)rows * c->post_tp * 2, s) != hipSuccess)
             return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
@@ -739,7 +791,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
-                       b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_diag, c->post_fast, idx,
+                       b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_fast, idx,
                        pn, c->post_ld);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post kernels launch failed");
 }
