@@ -351,21 +351,46 @@ __device__ __forceinline__ void lane_best(const uint32_t* crow32, const uint2* t
     }
 }
 
+// One template's overlap and denominator, and whether it counts (not a masked cc-* template).
+template <bool FAST>
+__device__ __forceinline__ bool lane_eval(const uint32_t* crow32, const uint2* tcs, int32_t t, uint32_t wf, int32_t lf,
+                                          bool cc, uint32_t& ov, int32_t& den) {
+    ov = crow32[t];
+    const uint2 pc = tcs[t];
+    const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
+                             (int32_t)(pc.x >> 31));
+    den = dice_den(c, wf, lf);
+    return !(c.w && cc);
+}
+
+// Matrix top-k: each lane also keeps its second best, so the first time a lane's template is
+// ranked its next candidate is that second one instead of a rescan of its templates from LDS
+// (a lane ranked twice still rescans)
+#ifndef POST_TOPK_SECOND
+#define POST_TOPK_SECOND 1
+#endif
+
 #ifndef POST_MATRIX_STORE
 #define POST_MATRIX_STORE 3
 #endif
 #define DICE_STR(x) #x
 #define DICE_UNROLL(n) _Pragma(DICE_STR(unroll n))
+// scoring loop unroll (A/B: 1, 2, 5, 10 within 1% for the matrix kernel; the match kernel
+// needs 57 instead of 64 VGPRs at 2)
 #ifndef SCORE_UNROLL
-#define SCORE_UNROLL 10
+#define SCORE_UNROLL kMatrix ? 10 : 2
 #endif
-// A pointer every lane holds the same value of, as SGPRs.
+// A global pointer every lane holds the same value of, as SGPRs (address space 1: an integer
+// round trip would leave a generic pointer, and generic stores are flat stores, which count in
+// lgkmcnt as well as vmcnt, so every LDS wait would also wait for them).
 template <class E>
-__device__ __forceinline__ E* uniform_ptr(E* p) {
+using gptr = __attribute__((address_space(1))) E*;
+template <class E>
+__device__ __forceinline__ gptr<E> uniform_ptr(E* p) {
     const uint64_t v = reinterpret_cast<uint64_t>(p);
     const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return reinterpret_cast<E*>(lo | (hi << 32));
+    return (gptr<E>)(lo | (hi << 32));
 }
 
 template <bool kMatrix, int TJ, bool FAST>
@@ -374,28 +399,44 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
                                              uint32_t* __restrict__ ov_out, double* __restrict__ score_out, int32_t k,
                                              uint32_t* __restrict__ mov, double* __restrict__ msc,
                                              int32_t* __restrict__ tki, double* __restrict__ tks, int lane) {
-    int32_t bi = -1, bd = 1;
-    uint32_t bo = 0;
+    int32_t bi = -1, bd = 1, bi2 = -1, bd2 = 1;
+    uint32_t bo = 0, bo2 = 0;
     // The file's row bases as SGPR values (readfirstlane: the compiler cannot fold a lane offset
     // into a hoisted per-lane 64-bit base) and the lane opaque per file: every store is SGPR base +
     // a 32-bit VGPR offset formed where it is used, so no per-lane address stays live across the
     // file loop (they spilled to scratch, and each reload's vmcnt(0) waited for every store
     // issued before it).
-    uint32_t* orow = nullptr;
-    double* srow = nullptr;
+    gptr<uint32_t> orow = nullptr;
+    gptr<double> srow = nullptr;
     uint32_t lo = (uint32_t)lane;
     if (kMatrix) {
         orow = uniform_ptr(mov + file * ld);
         srow = uniform_ptr(msc + file * ld);
         asm volatile("" : "+v"(lo));
     }
-    DICE_UNROLL(SCORE_UNROLL)
+    constexpr int kUnroll = SCORE_UNROLL;
+    DICE_UNROLL(kUnroll)
     for (int j = 0; j < TJ; ++j) {
         const int32_t t = (int32_t)lo + j * kWave;
         if (t < T) {
             uint32_t ov;
             int32_t den;
-            lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
+            if (kMatrix && POST_TOPK_SECOND) {
+                // the lane's two best (t ascending within a lane: a later template that ties takes
+                // the place, the strict (score, later key) order)
+                if (lane_eval<FAST>(crow32, tcs, t, wf, lf, cc, ov, den)) {
+                    const bool b1 = bi < 0 || ge<FAST>(ov, den, bo, bd);
+                    const bool b2 = !b1 && (bi2 < 0 || ge<FAST>(ov, den, bo2, bd2));
+                    bi2 = b1 ? bi : b2 ? t : bi2;
+                    bo2 = b1 ? bo : b2 ? ov : bo2;
+                    bd2 = b1 ? bd : b2 ? den : bd2;
+                    bi = b1 ? t : bi;
+                    bo = b1 ? ov : bo;
+                    bd = b1 ? den : bd;
+                }
+            } else {
+                lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
+            }
             if (kMatrix) {
 #if POST_MATRIX_STORE == 3
                 __builtin_nontemporal_store(ov, orow + t);
@@ -426,6 +467,7 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
         }
     } else if (tki) {
         uint32_t taken = 0;   // bit j: template lane + 64 j already ranked
+        bool second = true;   // (POST_TOPK_SECOND) the lane's second best not yet promoted
         for (int r = 0; r < k; ++r) {
             int32_t wi = bi, wd = bd;
             uint32_t wo = bo;
@@ -443,15 +485,23 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             }
             if (r + 1 < k && wi == bi) {   // the owner lane: next best among its untaken templates
                 taken |= 1u << (wi >> 6);
-                bi = -1;
-                bo = 0;
-                bd = 1;
-                for (int j = 0; j < TJ; ++j) {
-                    const int32_t t = lane + j * kWave;
-                    if (t < T && !((taken >> j) & 1u)) {
-                        uint32_t ov;
-                        int32_t den;
-                        lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
+                const bool promote = POST_TOPK_SECOND && second;
+                second = false;
+                if (promote) {
+                    bi = bi2;
+                    bo = bo2;
+                    bd = bd2;
+                } else {
+                    bi = -1;
+                    bo = 0;
+                    bd = 1;
+                    for (int j = 0; j < TJ; ++j) {
+                        const int32_t t = (int32_t)lo + j * kWave;
+                        if (t < T && !((taken >> j) & 1u)) {
+                            uint32_t ov;
+                            int32_t den;
+                            lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
+                        }
                     }
                 }
             }
