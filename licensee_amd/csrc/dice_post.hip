@@ -363,6 +363,16 @@ __device__ __forceinline__ bool lane_eval(const uint32_t* crow32, const uint2* t
     return !(c.w && cc);
 }
 
+// wave argmax: DPP row shifts (1) or the ds_bpermute butterfly (0)
+#ifndef POST_DPP_BEST
+#define POST_DPP_BEST 1
+#endif
+#if POST_DPP_BEST
+#define WAVE_BEST wave_best_dpp
+#else
+#define WAVE_BEST wave_best
+#endif
+
 // Matrix top-k: each lane also keeps its second best, so the first time a lane's template is
 // ranked its next candidate is that second one instead of a rescan of its templates from LDS
 // (a lane ranked twice still rescans)
@@ -458,7 +468,7 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
         }
     }
     if (!kMatrix) {
-        wave_best<FAST>(bi, bo, bd);
+        WAVE_BEST<FAST>(bi, bo, bd);
         if (lane == 0) {
             const double s = bi >= 0 ? dice_score(bo, bd) : 0.0;
             best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
@@ -471,7 +481,7 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
         for (int r = 0; r < k; ++r) {
             int32_t wi = bi, wd = bd;
             uint32_t wo = bo;
-            wave_best<FAST>(wi, wo, wd);
+            WAVE_BEST<FAST>(wi, wo, wd);
             if (lane == 0) {
                 tki[file * k + r] = wi;
                 tks[file * k + r] = wi >= 0 ? dice_score(wo, wd) : -1.0;

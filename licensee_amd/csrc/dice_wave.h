@@ -41,6 +41,36 @@ __device__ __forceinline__ void wave_best(int32_t& bi, uint32_t& bo, int32_t& bd
     }
 }
 
+// The same argmax by DPP (no LDS traffic: __shfl_xor is ds_bpermute): the row shifts and row
+// broadcasts of wave_incl_max, with lanes that have no source keeping the identity (index -1,
+// which never outranks), leave lane 63 with the best; it is then read back to every lane as
+// wave-uniform values. Every lane must be active. The order is a strict total order over the
+// candidates (distinct template indices), so the result is the butterfly's.
+template <bool FAST = false>
+__device__ __forceinline__ void wave_best_dpp(int32_t& bi, uint32_t& bo, int32_t& bd) {
+#define DICE_BEST_STEP(ctrl, rows)                                                                  \
+    {                                                                                               \
+        const int32_t oi = __builtin_amdgcn_update_dpp(-1, bi, ctrl, rows, 0xf, false);             \
+        const uint32_t oo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)bo, ctrl, rows, 0xf, false); \
+        const int32_t od = __builtin_amdgcn_update_dpp(1, bd, ctrl, rows, 0xf, false);              \
+        if (outranks_t<FAST>(oi, oo, od, bi, bo, bd)) {                                             \
+            bi = oi;                                                                                \
+            bo = oo;                                                                                \
+            bd = od;                                                                                \
+        }                                                                                           \
+    }
+    DICE_BEST_STEP(0x111, 0xf)   // row_shr:1
+    DICE_BEST_STEP(0x112, 0xf)   // row_shr:2
+    DICE_BEST_STEP(0x114, 0xf)   // row_shr:4
+    DICE_BEST_STEP(0x118, 0xf)   // row_shr:8
+    DICE_BEST_STEP(0x142, 0xa)   // row_bcast:15
+    DICE_BEST_STEP(0x143, 0xc)   // row_bcast:31
+#undef DICE_BEST_STEP
+    bi = __builtin_amdgcn_readlane(bi, kWave - 1);
+    bo = (uint32_t)__builtin_amdgcn_readlane((int32_t)bo, kWave - 1);
+    bd = __builtin_amdgcn_readlane(bd, kWave - 1);
+}
+
 // Inclusive prefix sum over the 64 lanes (DPP: row shifts within each 16-lane row, then the
 // row-15 / row-31 broadcasts); every lane must be active.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
