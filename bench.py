@@ -26,8 +26,9 @@ The JSON line also carries:
   parity       -- GPU results of the timed run vs the C oracle's hash mode: every rank checks a
                   sample of its own shard; checked files and mismatches are summed over ranks.
   extras.configs -- the other BASELINE configs (3: ~600 templates, bound-pruned match
-                  kernel, plus '3-allpairs': the same files on the postings kernel, which scores
-                  every pair; 4: long/mixed files; 5: full matrix + top-k) measured in the same
+                  kernel, plus '3-confidence': the same files through dice_batch_match_confidence
+                  (Dice#confidence: 0 without a match), and '3-allpairs': the same files on the
+                  postings kernel, which scores every pair; 4: long/mixed files; 5: full matrix + top-k) measured in the same
                   run (every rank, its own shard), each with its own HIP-event launch time, roofline
                   fraction, cpu_baseline and oracle parity sample.
 """
@@ -148,6 +149,7 @@ class Run:
         # the file bitset as the kernels read it: tile layout (T <= 64) or row-major rows (T > 64)
         in_bytes = self.batch.bytes_per_file() if self.kind != 3 else 8 * ((self.V + 63) // 64)
         self.algo_bytes_per_file = in_bytes + 4 + 4 + 1 + out_bytes
+        self.confidence = False   # dice_batch_match_confidence ('3-confidence')
 
     def step(self, sptr):
         if self.args.probe:
@@ -155,7 +157,7 @@ class Run:
         elif self.cfg == 5:
             self.batch.matrix(self.args.topk, sptr)
         else:
-            self.batch.match(self.args.threshold, sptr)
+            self.batch.match(self.args.threshold, sptr, confidence=self.confidence)
 
     def close(self):
         self.batch.close()
@@ -288,6 +290,8 @@ def parity_sample(run, orc, sptr, threads, n_sample):
         eb, eo, es = orc.match(f.bits[sl], f.wordset_size[sl], f.length[sl], f.cc_false_positive[sl],
                                run.args.threshold, nthreads=threads, mode=0)
         cpu_s = time.perf_counter() - t0
+        if run.confidence:   # Dice#confidence: 0 for a file without a match (dice.rb:51-53)
+            eo, es = np.where(eb >= 0, eo, 0), np.where(eb >= 0, es, 0.0)
         mism = int(np.sum(best[sl] != eb) + np.sum(ov[sl] != eo) + np.sum(score[sl] != es))
         return {'checked_files': sl.stop, 'mismatches': mism, 'oracle': 'oracle/dice_ref.c (hash Set#&)',
                 'oracle_files_per_s': sl.stop / cpu_s}
@@ -392,6 +396,10 @@ def measure_extra(r, c, args, stream, sptr, cpu, group):
                        'overlap bound can reach the top score are scored exactly (DESIGN.md 4); scores_per_s '
                        'counts decided pairs. 3-allpairs scores every pair')
         rec['deferred_files'] = int(group.reduce([r.batch.deferred(sptr)], 'sum')[0])
+    if r.confidence:
+        rec['note'] = ('dice_batch_match_confidence: Dice#match + #confidence as a caller reads them (dice.rb:8-14, '
+                       '51-53); a file without a match reports 0, so the bound-pruned kernel scores only '
+                       'templates that can reach the threshold. Same files as config 3')
     if not args.no_cpu_baseline:
         n_sample = {3: 20_000, 4: 30_000, 5: 50_000, '5-T600': 10_000}[c]
         threads = cpu['threads'] if group.rank == 0 else cpu['rank_threads']
@@ -442,6 +450,8 @@ def main():
                     choices=[2, 3, 4, 5, '5-T600'])
     ap.add_argument('--files-per-gpu', type=int, default=None)
     ap.add_argument('--threshold', type=float, default=98.0)
+    ap.add_argument('--confidence', action='store_true',
+                    help='match configs: dice_batch_match_confidence (Dice#confidence, 0 without a match)')
     ap.add_argument('--topk', type=int, default=3)
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU-work budget of the baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -504,6 +514,7 @@ def main():
     cfg = args.config
     n_per = args.files_per_gpu or DEFAULT_FILES[cfg]
     run = Run(cfg, n_per, rank, world, dev, nthreads, args)
+    run.confidence = bool(args.confidence) and cfg != 5
     matrix_mode = run.cfg == 5            # configs 5 and 5-T600: full matrix + top-k
     run_T_cfg3 = cfg in (3, '5-T600')     # config 3's template corpus
     stream = torch.cuda.Stream()          # a real (non-null) stream: kernels and HIP events share it
@@ -691,12 +702,14 @@ def main():
             r = Run(c, args.extra_files_per_gpu or DEFAULT_FILES[c], rank, world, dev, nthreads, args)
             variants = [(str(c), None)]
             if c == 3 and r.match_kernel == 4:
-                variants.append(('3-allpairs', {'DICE_POST_PRUNE': '0'}))
+                variants += [('3-confidence', 'confidence'), ('3-allpairs', {'DICE_POST_PRUNE': '0'})]
             for tag, env in variants:
-                saved = r.rescore(env, dev) if env else None
+                r.confidence = env == 'confidence'
+                saved = r.rescore(env, dev) if isinstance(env, dict) else None
                 extras['configs'][tag] = measure_extra(r, c, args, stream, sptr, cpu, group)
                 if saved:
                     r.restore(saved)
+            r.confidence = False
             r.close()
 
     if rank == 0:

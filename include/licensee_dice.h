@@ -108,6 +108,14 @@ int32_t dice_ctx_match_kernel(const dice_ctx *ctx);
  * Any of the three output pointers may be NULL. */
 int dice_match(dice_ctx *ctx, const dice_files *files, double threshold,
                int32_t *best, uint32_t *overlap, double *score);
+/* Dice#match and Dice#confidence exactly as a caller of the matcher sees them
+ * (dice.rb:8-14, 51-53): best[i] as dice_match; score[i] = Dice#confidence, i.e. the matched
+ * template's similarity, or 0.0 when best[i] == -1; overlap[i] the matched template's overlap or 0.
+ * The top-ranked template of an unmatched file is not computed, so the bound-pruned kernel
+ * (T > 64) drops every template whose bound is below the threshold from the start. Equal to
+ * dice_match's outputs on every matched file. */
+int dice_match_confidence(dice_ctx *ctx, const dice_files *files, double threshold,
+                          int32_t *best, uint32_t *overlap, double *score);
 
 /* Full N x T similarity matrix + per-file top-k (Dice#matches_by_similarity order).
  *   overlap/score: [n][T] row-major, every template (CC filter NOT applied), may be NULL;
@@ -167,6 +175,8 @@ int dice_batch_upload_ids(dice_batch *batch, int64_t n_files, const int64_t *off
  * bound-pruned kernel followed by the postings kernels over the files it deferred; their count
  * stays on the device. */
 int dice_batch_match(dice_batch *batch, double threshold, void *stream);
+/* dice_match_confidence's semantics for a device batch (same asynchrony and capture contract). */
+int dice_batch_match_confidence(dice_batch *batch, double threshold, void *stream);
 /* Introspection after dice_batch_match (synchronizes `stream`): files the bound-pruned kernel
  * deferred to the postings kernels in the last call (0 for other kernels). */
 int dice_batch_deferred(dice_batch *batch, int64_t *deferred, void *stream);

@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = (
     'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids', 'dice_last_gather_peer',
     'dice_batch_deferred',
     'dice_ctx_match_kernel', 'dice_exact_setup', 'dice_batch_exact', 'dice_batch_download_exact', 'dice_exact',
+    'dice_match_confidence', 'dice_batch_match_confidence',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -99,12 +100,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_ctx_info': (ctypes.c_int, [vp, vp, vp, vp, vp]),
         'dice_ctx_match_kernel': (ctypes.c_int32, [vp]),
         'dice_match': (ctypes.c_int, [vp, ctypes.POINTER(_Files), ctypes.c_double, vp, vp, vp]),
+        'dice_match_confidence': (ctypes.c_int, [vp, ctypes.POINTER(_Files), ctypes.c_double, vp, vp, vp]),
         'dice_similarity_matrix': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp, vp, i32, vp, vp]),
         'dice_batch_create': (ctypes.c_int, [vp, i64, ctypes.POINTER(vp)]),
         'dice_batch_destroy': (None, [vp]),
         'dice_batch_upload': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp]),
         'dice_batch_upload_ids': (ctypes.c_int, [vp, i64, vp, vp, i32, vp, vp, vp, vp]),
         'dice_batch_match': (ctypes.c_int, [vp, ctypes.c_double, vp]),
+        'dice_batch_match_confidence': (ctypes.c_int, [vp, ctypes.c_double, vp]),
         'dice_batch_matrix': (ctypes.c_int, [vp, i32, vp]),
         'dice_batch_download_match': (ctypes.c_int, [vp, vp, vp, vp, vp]),
         'dice_batch_download_matrix': (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
@@ -232,15 +235,19 @@ class Scorer:
         4 bound-pruned (dice_prune.hip)."""
         return int(load_library().dice_ctx_match_kernel(self._ctx))
 
-    def match(self, files: FileBatch, threshold: float):
+    def match(self, files: FileBatch, threshold: float, confidence: bool = False):
+        """(best, overlap, score) per file. confidence=False: score/overlap of the top-ranked
+        template even when it misses the threshold (dice_match); True: Dice#confidence, 0 for a
+        file without a match (dice_match_confidence, dice.rb:51-53)."""
         n = files.n
         best = np.empty(n, np.int32)
         ov = np.empty(n, np.uint32)
         score = np.empty(n, np.float64)
         if n:
             st = files._struct()
-            _check(load_library().dice_match(self._ctx, ctypes.byref(st), float(threshold),
-                                             _ptr(best), _ptr(ov), _ptr(score)))
+            lib = load_library()
+            fn = lib.dice_match_confidence if confidence else lib.dice_match
+            _check(fn(self._ctx, ctypes.byref(st), float(threshold), _ptr(best), _ptr(ov), _ptr(score)))
         return best, ov, score
 
     def matrix(self, files: FileBatch, k: int = 0):
@@ -331,8 +338,10 @@ class DeviceBatch:
                                                     stream or None))
         self.n = n
 
-    def match(self, threshold: float, stream: int = 0):
-        _check(load_library().dice_batch_match(self._b, float(threshold), stream or None))
+    def match(self, threshold: float, stream: int = 0, confidence: bool = False):
+        lib = load_library()
+        fn = lib.dice_batch_match_confidence if confidence else lib.dice_batch_match
+        _check(fn(self._b, float(threshold), stream or None))
 
     def matrix(self, k: int, stream: int = 0):
         _check(load_library().dice_batch_matrix(self._b, int(k), stream or None))

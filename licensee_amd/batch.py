@@ -70,12 +70,12 @@ class BatchDetector:
             b = self._device_batch(max(fb.n, 1))
             b.upload(fb)
             b.exact(fmask)
-            b.match(float(thr))
+            b.match(float(thr), confidence=True)
             exact = b.download_exact()
             best, _, score = b.download_match()
         else:
             fb, copyright, exact, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads)
-            best, _, score = self.engine.scorer.match(fb, float(thr))
+            best, _, score = self.engine.scorer.match(fb, float(thr), confidence=True)
         templates = self.engine.templates
         no_license, other = License.find('no-license'), License.find('other')
         out = []

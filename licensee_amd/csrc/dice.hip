@@ -489,7 +489,7 @@ void dice_batch_destroy(dice_batch* b) {
     }
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
                     b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
-                    b->d_defer, b->d_ndefer, b->d_exact, b->d_fmask};
+                    b->d_defer, b->d_ndefer, b->d_exact, b->d_fmask, b->d_qctr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -513,6 +513,16 @@ int dice_batch_create(dice_ctx* ctx, int64_t capacity, dice_batch** out) {
         (ctx->prune && (rc = dice::prune_reserve(ctx, b)))) {
         dice_batch_destroy(b);
         return rc;
+    }
+    if (ctx->kind == 1 && ctx->prog.queue) {
+        if ((rc = dalloc(&b->d_qctr, 1))) {
+            dice_batch_destroy(b);
+            return rc;
+        }
+        if (hipMemset(b->d_qctr, 0, 4) != hipSuccess) {
+            dice_batch_destroy(b);
+            return fail(DICE_E_DEVICE, "hipMemset failed");
+        }
     }
     *out = b;
     return DICE_OK;
@@ -622,7 +632,20 @@ int dice_batch_upload_ids(dice_batch* b, int64_t n, const int64_t* offsets, cons
     return upload_tail(b, n, wordset_size, length, cc, s);
 }
 
-int dice_batch_match(dice_batch* b, double thr, void* stream) {
+}  // extern "C"
+
+// Dice#confidence for the files dice_batch_match left without a match: overlap 0 and score 0.0
+// (dice.rb:52-54: confidence is 0 when match is nil).
+__global__ __launch_bounds__(256) void dice_confidence_outputs(const int32_t* __restrict__ best, uint32_t* __restrict__ ov,
+                                                               double* __restrict__ score, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n && best[i] < 0) {
+        ov[i] = 0;
+        score[i] = 0.0;
+    }
+}
+
+static int batch_match(dice_batch* b, double thr, void* stream, bool confidence) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
     dice_ctx* c = b->ctx;
     if (b->n == 0) return DICE_OK;
@@ -637,7 +660,7 @@ int dice_batch_match(dice_batch* b, double thr, void* stream) {
         int rc = dice::lds_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else if (c->kind == 3) {
-        int rc = c->prune ? dice::prune_launch_match(c, b, thr, s) : dice::post_launch_match(c, b, thr, s);
+        int rc = c->prune ? dice::prune_launch_match(c, b, thr, s, confidence) : dice::post_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
@@ -645,8 +668,19 @@ int dice_batch_match(dice_batch* b, double thr, void* stream) {
                            b->d_ov, b->d_score);
     }
     HIP_TRY(hipGetLastError());
+    if (confidence) {
+        hipLaunchKernelGGL(dice_confidence_outputs, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0, s, b->d_best,
+                           b->d_ov, b->d_score, b->n);
+        HIP_TRY(hipGetLastError());
+    }
     return DICE_OK;
 }
+
+extern "C" {
+
+int dice_batch_match(dice_batch* b, double thr, void* stream) { return batch_match(b, thr, stream, false); }
+
+int dice_batch_match_confidence(dice_batch* b, double thr, void* stream) { return batch_match(b, thr, stream, true); }
 
 static int ensure_matrix(dice_batch* b, int32_t k) {
     dice_ctx* c = b->ctx;
@@ -915,13 +949,14 @@ int small_upload(dice_ctx* c, dice_batch* b, const dice_files* f, const SmallLay
     return DICE_OK;
 }
 
-int small_match(dice_ctx* c, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
+int small_match(dice_ctx* c, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score,
+                bool confidence) {
     DeviceGuard g(c->device);
     dice_batch* b = nullptr;
     int rc;
     if ((rc = small_batch(c, &b))) return rc;
     const SmallLayout L = small_layout(c);
-    if ((rc = small_upload(c, b, f, L)) || (rc = dice_batch_match(b, thr, nullptr))) return rc;
+    if ((rc = small_upload(c, b, f, L)) || (rc = batch_match(b, thr, nullptr, confidence))) return rc;
     const size_t n = (size_t)f->n_files;
     HIP_TRY(hipMemcpyAsync(c->h_small_out, b->d_out, L.score + n * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -987,19 +1022,29 @@ int small_matrix(dice_ctx* c, const dice_files* f, uint32_t* ov, double* score, 
 
 extern "C" {
 
-int dice_match(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
+static int host_match(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score,
+                      bool confidence) {
     if (!ctx || !f) return fail(DICE_E_ARG, "NULL ctx/files");
     if (f->n_files == 0) return DICE_OK;
     if (f->n_files < 0) return fail(DICE_E_ARG, "n_files < 0");
     if (!f->bits || !f->wordset_size || !f->length || !f->cc_false_positive)
         return fail(DICE_E_ARG, "NULL file arrays");
-    if (f->n_files <= kSmallFiles && !getenv_flag("DICE_NO_SMALL_CALL")) return small_match(ctx, f, thr, best, ov, score);
+    if (f->n_files <= kSmallFiles && !getenv_flag("DICE_NO_SMALL_CALL"))
+        return small_match(ctx, f, thr, best, ov, score, confidence);
     dice_batch* b = nullptr;
     int rc = dice::scratch_for(ctx, f->n_files, &b);
     if (rc) return rc;
     if ((rc = dice_batch_upload(b, f, nullptr))) return rc;
-    if ((rc = dice_batch_match(b, thr, nullptr))) return rc;
+    if ((rc = batch_match(b, thr, nullptr, confidence))) return rc;
     return dice_batch_download_match(b, best, ov, score, nullptr);
+}
+
+int dice_match(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
+    return host_match(ctx, f, thr, best, ov, score, false);
+}
+
+int dice_match_confidence(dice_ctx* ctx, const dice_files* f, double thr, int32_t* best, uint32_t* ov, double* score) {
+    return host_match(ctx, f, thr, best, ov, score, true);
 }
 
 int dice_similarity_matrix(dice_ctx* ctx, const dice_files* f, uint32_t* ov, double* score, int32_t k,

@@ -121,7 +121,7 @@ int post_launch_match_indexed(dice_ctx* c, dice_batch* b, double thr, const int3
 // the batch's dense-partial buffer ([capacity][tp] u16)
 int post_reserve(dice_ctx* c, dice_batch* b);
 int prune_setup(dice_ctx* c, const dice_templates* t);
-int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bool confidence = false);
 // the pruned match's device buffers for batch b (called by dice_batch_create)
 int prune_reserve(dice_ctx* c, dice_batch* b);
 // dice_batch_upload's tail (scalars, repack) for rows already copied to b->d_rows on `s`
@@ -174,4 +174,6 @@ struct dice_batch {
     uint64_t* d_fmask = nullptr;
     // small-call batch: d_wf/d_len/d_cc/d_rows carved from d_in, results from d_out
     void *d_in = nullptr, *d_out = nullptr;
+    // sparse program's tile queue (kind 1 with DICE_PROG_QUEUE=1): next-tile counter, 0 between launches
+    uint32_t* d_qctr = nullptr;
 };

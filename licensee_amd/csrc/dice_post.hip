@@ -51,6 +51,22 @@ namespace dice {
 #ifndef POST_DIAG
 #define POST_DIAG 0
 #endif
+// Dense partials: u8 rows ([n][tp] bytes) for files whose every prefix overlap fits a byte, u16
+// rows ([n][tp]) and a per-file flag for the others (about one config-3 file in seven: a prefix
+// of 1024 words can hold 600 of one template's). POST_PARTIALS_U8=0 writes every row as u16 (A/B).
+#ifndef POST_PARTIALS_U8
+#define POST_PARTIALS_U8 1
+#endif
+struct Partials {
+    uint16_t* p16;   // [n][tp] u16 rows (files flagged 1)
+    uint32_t* p8;    // [n][tp / 4] u32 words of four u8 partials (files flagged 0)
+    uint8_t* flag;   // [n] 1: the file's row is the u16 one
+};
+
+// A/B: the dense kernel's file prefixes staged through LDS by coalesced loads (1) or loaded per lane (0)
+#ifndef POST_DENSE_LDS_PREFIX
+#define POST_DENSE_LDS_PREFIX 1
+#endif
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
@@ -160,7 +176,7 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
 template <int DP, int TPMAX>
 __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(TPMAX <= 608 ? 8 : 4, TPMAX <= 608 ? 8 : 4))) void dice_post_dense(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
-    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ dense, const int32_t* __restrict__ idx,
+    const uint64_t* __restrict__ dmask, Partials pt, const int32_t* __restrict__ idx,
     const uint32_t* __restrict__ pn) {
     __shared__ uint32_t stage32[kPostFiles * (TPMAX + 2) / 2];   // <= 78 KiB at TPMAX 608: 2 per CU
     uint16_t* st = reinterpret_cast<uint16_t*>(stage32);
@@ -171,13 +187,37 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     // rows[idx[i]] (persistent grid, count read on the device); partials stay indexed by i
     const int64_t nn = idx ? (int64_t)*pn : n;
     for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
-    {
+    // the tile's file prefixes, staged through LDS: thread (file tid / 16, word tid % 16) loads one
+    // u64 (each file's 128 B are one coalesced segment), then every wave reads its lanes' words
+    // back. (Loaded per lane, each wave fetched all 64 files' prefixes with 16 loads of 64
+    // scattered 8-byte pieces: 16 waves x 1024 L1 requests per tile.) Rows padded to 18 words:
+    // lane l's 16-byte reads start at bank 36 l mod 64, conflict-free within each 16-lane group.
+    constexpr int kPreStride = kPostMaxDense + 2;
+    static_assert(kPostFiles * kPostMaxDense == kPostWaves * kWave, "one prefix word per thread");
+    static_assert(kPostFiles * kPreStride * 2 <= kPostFiles * (TPMAX + 2) / 2, "prefixes fit the stage");
+    uint64_t fd[DP];
+    if (POST_DENSE_LDS_PREFIX) {
+        {
+            uint64_t* pre = reinterpret_cast<uint64_t*>(stage32);
+            const int fi = (int)threadIdx.x / kPostMaxDense, d = (int)threadIdx.x % kPostMaxDense;
+            const int64_t file = f0 + fi;
+            uint64_t v = 0;
+            if (file < nn && d < D) v = rows[(idx ? (int64_t)idx[file] : file) * w64 + d];
+            pre[fi * kPreStride + d] = v;
+        }
+        __syncthreads();
+        const uint64_t* pre = reinterpret_cast<const uint64_t*>(stage32) + lane * kPreStride;
+#pragma unroll
+        for (int d = 0; d < DP; ++d) fd[d] = pre[d];
+        __syncthreads();   // every wave holds its prefixes before the partials overwrite the stage
+    } else {
         const int64_t file = f0 + lane;
         const bool valid = file < nn;
         const int64_t rf = valid && idx ? (int64_t)idx[file] : file;
-        uint64_t fd[DP];
 #pragma unroll
         for (int d = 0; d < DP; ++d) fd[d] = (valid && d < D) ? rows[rf * w64 + d] : 0;
+    }
+    {
         const int32_t tw = (T + kPostWaves - 1) / kPostWaves;
         const int32_t tb = wave * tw, te = min(T, tb + tw);
         uint16_t* crow = st + lane * cs;
@@ -219,22 +259,67 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
         const int64_t file = f0 + fi;
         if (file >= nn) break;
         const uint32_t* src = stage32 + (fi * cs) / 2;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(dense + file * tp);
-        for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
+        // a byte row when every partial of the file fits a byte (one wave-wide vote), else u16
+        bool wide = !POST_PARTIALS_U8;
+        if (POST_PARTIALS_U8) {
+            bool any = false;
+            for (int32_t j = lane; j < tp / 2; j += kWave) any |= (src[j] & 0xFF00FF00u) != 0;
+            wide = __ballot(any) != 0;
+            if (lane == 0) pt.flag[file] = wide ? 1 : 0;
+        }
+        if (!wide) {
+            uint32_t* dst = pt.p8 + file * (tp / 4);
+            // bytes 0 and 2 of each u16 pair: v_perm_b32 packs four partials into one word
+            for (int32_t j = lane; j < tp / 4; j += kWave)
+                dst[j] = __builtin_amdgcn_perm(src[2 * j + 1], src[2 * j], 0x06040200u);
+        } else {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(pt.p16 + file * tp);
+            for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
+        }
     }
     __syncthreads();   // the stage is refilled by the next tile
     }
 }
 
-// The file's dense partials into its counter row (a plain copy, u16 pairs widened: this wave's
-// postings adds for the file come after it; the copy writes every entry, so the row is never
-// re-zeroed), one LDS address and immediate offsets.
+// The file's dense partials into its counter row (a plain copy, widened: this wave's postings
+// adds for the file come after it; the copy writes every entry, so the row is never re-zeroed),
+// one LDS address and immediate offsets. wide (uniform): part[] holds u16 pairs, else words of
+// four u8 partials (one 16-byte LDS store each).
 template <int PJ>
-__device__ __forceinline__ void copy_in(uint32_t* crow32, const uint32_t (&part)[PJ], int32_t tp, int lane) {
-    uint2* dst = reinterpret_cast<uint2*>(crow32) + lane;
+__device__ __forceinline__ void copy_in(uint32_t* crow32, const uint32_t (&part)[PJ], int32_t tp, bool wide, int lane) {
+    if (wide) {
+        uint2* dst = reinterpret_cast<uint2*>(crow32) + lane;
 #pragma unroll
-    for (int j = 0; j < PJ; ++j)
-        if (lane + j * kWave < tp / 2) dst[j * kWave] = make_uint2(part[j] & 0xFFFFu, part[j] >> 16);
+        for (int j = 0; j < PJ; ++j)
+            if (lane + j * kWave < tp / 2) dst[j * kWave] = make_uint2(part[j] & 0xFFFFu, part[j] >> 16);
+    } else {
+        uint4* dst = reinterpret_cast<uint4*>(crow32) + lane;
+#pragma unroll
+        for (int j = 0; j < (PJ + 1) / 2; ++j) {
+            const uint32_t v = part[j];
+            if (lane + j * kWave < tp / 4) dst[j * kWave] = make_uint4(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, v >> 24);
+        }
+    }
+}
+
+// A file's partials (u16 pairs or u8 quads, see copy_in). CLAMP: unconditional loads at clamped
+// indices (copy_in masks the rest), else exec-masked ones.
+template <int PJ, bool CLAMP>
+__device__ __forceinline__ void load_partials(const Partials& pt, int64_t pos, int32_t tp, bool wide, int lane,
+                                              uint32_t (&part)[PJ]) {
+    const uint32_t* src = wide ? reinterpret_cast<const uint32_t*>(pt.p16 + pos * tp) : pt.p8 + pos * (tp / 4);
+    const int32_t nw = wide ? tp / 2 : tp / 4;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+        const int32_t i = lane + j * kWave;
+        if (!wide && j >= (PJ + 1) / 2) {
+            part[j] = 0;
+        } else if (CLAMP) {
+            part[j] = src[min(i, nw - 1)];
+        } else {
+            part[j] = i < nw ? src[i] : 0;
+        }
+    }
 }
 
 __device__ __forceinline__ void load_chunks(const uint64_t* __restrict__ row, int32_t w64, int32_t pb, int lane,
@@ -297,7 +382,8 @@ __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int3
 // afford them.
 template <int WCAP, bool LATE, int PJ>
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
-                                              const uint32_t* __restrict__ psrc, int32_t tp, uint32_t* wq, uint2* lq,
+                                              const Partials& pt, int64_t pos, bool wide, int32_t tp, uint32_t* wq,
+                                              uint2* lq,
                                               const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
                                               uint32_t* crow32, int lane) {
     uint32_t nq = 0;           // queued narrow words (wave-uniform)
@@ -309,11 +395,9 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
     uint64_t xs[kChunks];
     if (LATE) {
         uint32_t part[PJ];
-        // unconditional loads at clamped indices: copy_in masks the pairs past tp / 2
-#pragma unroll
-        for (int j = 0; j < PJ; ++j) part[j] = psrc[min(lane + j * kWave, tp / 2 - 1)];
+        load_partials<PJ, true>(pt, pos, tp, wide, lane, part);
         if (pb < w64) load_chunks(row, w64, pb, lane, xs);
-        copy_in<PJ>(crow32, part, tp, lane);
+        copy_in<PJ>(crow32, part, tp, wide, lane);
         if (pb < w64) {
             queue_chunks<WCAP>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
             pb += kChunks * kWave;
@@ -540,19 +624,6 @@ __device__ __forceinline__ void score_file(uint32_t* crow32, const uint2* tcs, i
 template <int TPMAX>
 constexpr int pairs_per_lane() { return (TPMAX / 2 + kWave - 1) / kWave; }   // u32 partial pairs per lane
 
-// A file's dense partials, loaded while the wave is still scoring the previous file (match
-// mode), so they are in flight during that file's scoring instead of heading this file's chain.
-template <int PJ>
-__device__ __forceinline__ void prefetch_partials(const uint16_t* __restrict__ dense, int64_t pos, int32_t tp,
-                                                  int lane, uint32_t (&part)[PJ]) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(dense + pos * tp);
-#pragma unroll
-    for (int j = 0; j < PJ; ++j) {
-        const int32_t i = lane + j * kWave;
-        part[j] = i < tp / 2 ? src[i] : 0;
-    }
-}
-
 // Phases 2 + 3, one file per wave (16 waves x 4 files per workgroup). Each wave owns one u32
 // counter row in LDS (zero between files). Narrow words are queued from the file's u64 words
 // >= D and walked (walk_short / walk_long) after the file's dense partials (from
@@ -561,7 +632,7 @@ __device__ __forceinline__ void prefetch_partials(const uint16_t* __restrict__ d
 template <bool kMatrix, int KM, int TPMAX>
 __device__ __forceinline__ void post_narrow_body(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
-    const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+    const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
@@ -608,8 +679,12 @@ __device__ __forceinline__ void post_narrow_body(
         asm volatile("" : "+v"(lw));   // the slot address formed here, not hoisted out of the tile loop
         if ((lw & (kPostWaves - 1)) == (uint32_t)wave) tsc[wave][lw >> 4] = make_uint2(twf, tlen);
     }
-    uint32_t pre[kPJ];   // match mode: the next file's dense partials (prefetched)
-    if (!kMatrix && wave < nt) prefetch_partials<kPJ>(dense, f0 + wave, tp, lane, pre);
+    // the tile's partial formats (bit l: position f0 + l has a u16 row)
+    const uint64_t tov = POST_PARTIALS_U8 ? __ballot(pt.flag[f0 + min(lane, nt - 1)] != 0) : ~0ull;
+    // match mode: the next file's dense partials, prefetched while the wave scores the previous
+    // file (the matrix kernel loads them at the file's start: file_postings LATE)
+    uint32_t pre[kPJ];
+    if (!kMatrix && wave < nt) load_partials<kPJ, false>(pt, f0 + wave, tp, (tov >> wave) & 1, lane, pre);
     for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
         const int64_t pos = f0 + fi;
         if (fi >= nt) break;   // wave-uniform
@@ -622,7 +697,8 @@ __device__ __forceinline__ void post_narrow_body(
         int lanef = lane;   // likewise every lane-derived constant (lane + 64 j, lane addresses)
         if (kMatrix) asm volatile("" : "+s"(Tf), "+s"(tpf), "+s"(ldf), "+v"(lanef));
         // this file's dense partials start its counter row (matrix mode: inside file_postings)
-        if (!kMatrix) copy_in<kPJ>(crow32, pre, tpf, lanef);
+        const bool wide = (tov >> fi) & 1;
+        if (!kMatrix) copy_in<kPJ>(crow32, pre, tpf, wide, lanef);
         uint32_t wf;
         int32_t lf;
         if (kMatrix) {
@@ -634,10 +710,11 @@ __device__ __forceinline__ void post_narrow_body(
             lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
         }
         const bool cc = ((tcc >> fi) & 1u) != 0;
-        file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, reinterpret_cast<const uint32_t*>(dense + pos * tpf), tpf,
-                                           wq[wave], lq[wave], prow, plong, crow32, lanef);
+        file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow, plong, crow32,
+                                           lanef);
         // match mode: the wave's next file's partials fly while this one is scored
-        if (!kMatrix && fi + kPostWaves < nt) prefetch_partials<kPJ>(dense, pos + kPostWaves, tpf, lane, pre);
+        if (!kMatrix && fi + kPostWaves < nt)
+            load_partials<kPJ, false>(pt, pos + kPostWaves, tpf, (tov >> (fi + kPostWaves)) & 1, lane, pre);
 
         if (POST_DIAG & 8) continue;
         score_file<kMatrix, KM, kTJ>(crow32, tcs, Tf, ldf, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
@@ -651,13 +728,13 @@ __device__ __forceinline__ void post_narrow_body(
 template <int TPMAX>
 __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_narrow_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
-    const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+    const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
-    post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+    post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, pt, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
@@ -669,13 +746,13 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 template <int KM, int TPMAX>
 __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(POST_MATRIX_OCC, POST_MATRIX_OCC))) void dice_post_narrow_matrix(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
-    const uint16_t* __restrict__ dense, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
+    const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
     const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
-    post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, dense, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+    post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, pt, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
@@ -801,17 +878,29 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
+// The batch's partials region: [capacity][tp] u16 rows | [capacity][tp] u8 rows | [capacity] flags.
+static Partials partials_of(const dice_ctx* c, const dice_batch* b) {
+    char* base = reinterpret_cast<char*>(b->d_pdense);
+    const size_t n16 = (size_t)b->capacity * c->post_tp * 2, n8 = (size_t)b->capacity * c->post_tp;
+    Partials pt;
+    pt.p16 = reinterpret_cast<uint16_t*>(base);
+    pt.p8 = reinterpret_cast<uint32_t*>(base + n16);
+    pt.flag = reinterpret_cast<uint8_t*>(base + n16 + n8);
+    return pt;
+}
+
 template <int DP>
 static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t groups, const int32_t* idx,
                          const uint32_t* pn) {
     auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
-                       (const uint64_t*)c->d_pdm, (uint16_t*)b->d_pdense, idx, pn);
+                       (const uint64_t*)c->d_pdm, partials_of(c, b), idx, pn);
 }
 
 int post_reserve(dice_ctx* c, dice_batch* b) {
-    const size_t need = (size_t)b->capacity * c->post_tp * 2;
+    // u16 rows, u8 rows and flags (partials_of); the u16 region is only touched for flagged files
+    const size_t need = (size_t)b->capacity * c->post_tp * 3 + (size_t)b->capacity;
     if (b->pdense_bytes < need) {
         if (b->d_pdense) (void)hipFree(b->d_pdense);
         b->d_pdense = nullptr;
@@ -833,10 +922,15 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     const int64_t tiles = (b->n + kPostFiles - 1) / kPostFiles;
     // two workgroups per CU are resident in either kernel (LDS)
     const int64_t groups = idx ? std::min<int64_t>(tiles, 2 * (int64_t)c->n_cu) : tiles;
+    const Partials pt = partials_of(c, b);
     if (c->post_dense == 0 || (POST_DIAG & 1)) {
-        const int64_t rows = idx ? b->capacity : b->n;
-        if (hipMemsetAsync(b->d_pdense, 0, (size_t)rows * c->post_tp * 2, s) != hipSuccess)
-            return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
+        // no dense prefix: zero partials (u8 rows with flags 0; u16 rows when every row is u16)
+        const size_t rows = (size_t)(idx ? b->capacity : b->n);
+        const hipError_t e = POST_PARTIALS_U8
+                                 ? (hipMemsetAsync(pt.p8, 0, rows * c->post_tp, s) == hipSuccess
+                                        ? hipMemsetAsync(pt.flag, 0, rows, s) : hipErrorUnknown)
+                                 : hipMemsetAsync(pt.p16, 0, rows * c->post_tp * 2, s);
+        if (e != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
     } else {
         switch ((c->post_dense + 3) / 4) {
             case 1: launch_dense<4>(c, b, s, groups, idx, pn); break;
@@ -849,7 +943,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
                                   : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad> : dice_post_narrow_match<kPostMaxTpad>);
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
-                       (const uint16_t*)b->d_pdense, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
+                       pt, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
                        b->d_mov, b->d_mscore, k > 0 ? b->d_tki : nullptr, b->d_tks, c->post_fast, idx,
                        pn, c->post_ld);

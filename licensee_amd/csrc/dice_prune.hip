@@ -147,7 +147,8 @@ __device__ __forceinline__ void score_template(int32_t ts, int32_t to, const Rec
         bi = to;
         bo = ov;
         bd = den;
-        llo = (float)bo * __builtin_amdgcn_rcpf((float)bd) * kLloScale;
+        // (never below its starting value: the confidence mode's threshold floor)
+        llo = fmaxf(llo, (float)bo * __builtin_amdgcn_rcpf((float)bd) * kLloScale);
     }
 }
 
@@ -248,7 +249,7 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
     __builtin_amdgcn_wave_barrier();   // the row (written above) is read by other lanes below
     const uint32_t K1 = rfl(__builtin_amdgcn_readlane(wave_incl_max(ks), kWave - 1));
     PHASE(2);
-    if ((K1 & ~kKeyLow) != 0) {
+    if ((K1 & ~kKeyLow) != 0 && !(__uint_as_float(K1 & ~kKeyLow) < llo)) {
         int32_t l1;
         const int32_t t1 = key_template(K1, ks, l1);
         if (PRUNE_DIAG & 2) {
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
     int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast,
     bool zero_base, uint32_t wf_noclamp, int32_t* __restrict__ defer, uint32_t* __restrict__ ndefer,
-    int32_t max_evals, int32_t route_cands, uint64_t* __restrict__ diag_out) {
+    int32_t max_evals, int32_t route_cands, float llo0, uint64_t* __restrict__ diag_out) {
     constexpr int kTP = TJ * kWave;
     // route_cands packs the routing point: candidates | exact scores before the test << 16 (0: 2)
     const int32_t route_at = (route_cands >> 16) ? (route_cands >> 16) : 2;
@@ -407,7 +408,9 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                 const uint64_t below = __ballot(lane < TJ && (int32_t)sb.x <= lfi);
                 const int32_t jstar = below ? 63 - (int32_t)__builtin_clzll(below) : 0;
                 const bool fast = corpus_fast && wf < (1u << 20) && lf < (1u << 21);
-                float llo = -1.0f;
+                // llo0: -1 (the exact top score of every file), or the confidence mode's threshold
+                // floor (only templates that can reach the threshold are scored)
+                float llo = llo0;
                 uint32_t key[TJ], lmax;
                 PHASE(1);
                 if (!big && !ccf && wf >= wf_noclamp)
@@ -641,7 +644,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
 }
 
 template <int J, int TJ>
-static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0) {
     constexpr int NW = kPruneWaves;
     const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
     auto kern = dice_prune4<J, TJ, NW>;
@@ -675,7 +678,7 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows, b->n,
                        per_wave, c->w64, c->T, pa, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score,
                        c->post_fast, c->prune_zero_base, c->prune_wf_noclamp, b->d_defer, b->d_ndefer, max_evals,
-                       route, diag);
+                       route, llo0, diag);
     if ((PRUNE_DIAG & 8) && diag) {
         // diagnostic build only: per-phase shader-clock totals over all waves, per file
         std::vector<uint64_t> h((size_t)groups * NW * (kTPhases + 1));
@@ -692,14 +695,14 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
 }
 
 template <int J>
-static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0) {
     switch (prune_tj(c->T)) {
-        case 2: return launch_prune<J, 2>(c, b, thr, s);
-        case 4: return launch_prune<J, 4>(c, b, thr, s);
-        case 6: return launch_prune<J, 6>(c, b, thr, s);
-        case 8: return launch_prune<J, 8>(c, b, thr, s);
-        case 10: return launch_prune<J, 10>(c, b, thr, s);
-        default: return launch_prune<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s);
+        case 2: return launch_prune<J, 2>(c, b, thr, s, llo0);
+        case 4: return launch_prune<J, 4>(c, b, thr, s, llo0);
+        case 6: return launch_prune<J, 6>(c, b, thr, s, llo0);
+        case 8: return launch_prune<J, 8>(c, b, thr, s, llo0);
+        case 10: return launch_prune<J, 10>(c, b, thr, s, llo0);
+        default: return launch_prune<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s, llo0);
     }
 }
 
@@ -716,19 +719,25 @@ int prune_reserve(dice_ctx* c, dice_batch* b) {
 // Dice#match over the batch, asynchronous on `s`: the pruned kernel, then the postings kernels
 // over the files it deferred (their count stays on the device: persistent grids read it and
 // exit at once when it is 0).
-int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+//
+// confidence (dice_batch_match_confidence: Dice#match + #confidence, dice.rb:8-14,52-54): a file
+// that matches nothing reports confidence 0, not its top score, so only templates that can reach
+// the threshold need an exact score -- the drop level starts at the threshold (keys are in units
+// of score / 400; the 2^-11 margin covers the keys' f32 evaluation as for the best score).
+int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bool confidence) {
     if (b->n == 0) return DICE_OK;
     int rc;
     if ((rc = prune_reserve(c, b))) return rc;
     if (hipMemsetAsync(b->d_ndefer, 0, 4, s) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
+    const float llo0 = confidence && thr > 0 ? (float)(thr / 400.0 * (1.0 - 1.0 / 2048)) : -1.0f;
     switch ((c->w64 + kWave - 1) / kWave) {
-        case 1: rc = launch_prune_j<1>(c, b, thr, s); break;
-        case 2: rc = launch_prune_j<2>(c, b, thr, s); break;
+        case 1: rc = launch_prune_j<1>(c, b, thr, s, llo0); break;
+        case 2: rc = launch_prune_j<2>(c, b, thr, s, llo0); break;
         case 3:
-        case 4: rc = launch_prune_j<4>(c, b, thr, s); break;
+        case 4: rc = launch_prune_j<4>(c, b, thr, s, llo0); break;
         case 5:
-        case 6: rc = launch_prune_j<6>(c, b, thr, s); break;
-        default: rc = launch_prune_j<8>(c, b, thr, s); break;
+        case 6: rc = launch_prune_j<6>(c, b, thr, s, llo0); break;
+        default: rc = launch_prune_j<8>(c, b, thr, s, llo0); break;
     }
     if (rc) return rc;
     return post_launch_match_indexed(c, b, thr, b->d_defer, b->d_ndefer, s);

@@ -60,7 +60,7 @@ class DiceEngine:
     def match_files(self, files: Sequence, threshold=None):
         """Batched ``Dice#match``/``#confidence``: list of (License or None, confidence)."""
         thr = config.confidence_threshold() if threshold is None else threshold
-        best, _, score = self.scorer.match(self.intern(files), float(thr))
+        best, _, score = self.scorer.match(self.intern(files), float(thr), confidence=True)
         return [(self.templates[b], s) if b >= 0 else (None, 0) for b, s in zip(best.tolist(), score.tolist())]
 
 

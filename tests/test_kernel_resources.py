@@ -1,0 +1,40 @@
+"""Register budgets of the T > 64 kernels, from the compiler's resource remarks (no GPU needed).
+
+The postings kernels and the config-3 pruned kernel are written for 8 waves per SIMD (64 VGPRs,
+two 16-wave workgroups per CU). A kernel that spills to scratch pays a reload whose vmcnt(0) waits
+for every store and load issued before it ("Matrix kernel without spills"): keep
+them at zero scratch and full occupancy."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'tools'))
+
+HIPCC = '/opt/rocm/bin/hipcc'
+
+
+def _resources(src):
+    from kernel_resources import kernel_resources
+    rows = kernel_resources(os.path.join(ROOT, 'licensee_amd', 'csrc', src))
+    assert rows, 'no resource remarks (did the compile fail?)'
+    return {r['name']: r for r in rows}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
+def test_postings_kernels_fit_8_waves_without_scratch():
+    res = _resources('dice_post.hip')
+    for name in ('dice_post_narrow_match<608>', 'dice_post_narrow_matrix<1, 608>', 'dice_post_dense<16, 608>',
+                 'dice_post_narrow_match<704>', 'dice_post_narrow_matrix<1, 704>'):
+        r = next(v for k, v in res.items() if k.endswith('dice::' + name))
+        assert r['ScratchSize [bytes/lane]'] == '0', (name, r)
+        assert r['VGPRs Spill'] == '0', (name, r)
+        assert int(r['Occupancy [waves/SIMD]']) == 8, (name, r)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
+def test_config3_pruned_kernel_fits_8_waves_without_scratch():
+    res = _resources('dice_prune.hip')
+    r = next(v for k, v in res.items() if k.endswith('dice::dice_prune4<6, 10, 16>'))   # V = 23,494, T = 600
+    assert r['ScratchSize [bytes/lane]'] == '0' and int(r['Occupancy [waves/SIMD]']) == 8, r

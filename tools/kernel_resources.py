@@ -3,17 +3,19 @@
 
     python tools/kernel_resources.py licensee_amd/csrc/dice_prune.hip [name-filter]
 """
+import os
 import re
 import subprocess
 import sys
+import tempfile
 
 
-def main():
-    src = sys.argv[1]
-    filt = sys.argv[2] if len(sys.argv) > 2 else ''
-    out = subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-c', '-o',
-                          '/tmp/_kr.o', src, '-Rpass-analysis=kernel-resource-usage'],
-                         capture_output=True, text=True).stderr
+def kernel_resources(src, extra_flags=()):
+    """[{name, VGPRs, TotalSGPRs, SGPRs Spill, VGPRs Spill, ScratchSize [bytes/lane], Occupancy ...}] per kernel."""
+    with tempfile.TemporaryDirectory() as d:
+        out = subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-c', '-o',
+                              os.path.join(d, 'kr.o'), src, '-Rpass-analysis=kernel-resource-usage', *extra_flags],
+                             capture_output=True, text=True).stderr
     cur = None
     rows = []
     for line in out.splitlines():
@@ -32,7 +34,13 @@ def main():
         elif cur is not None and ':' in txt:
             k, v = txt.split(':', 1)
             cur[k.strip()] = v.strip()
-    for r in rows:
+    return rows
+
+
+def main():
+    src = sys.argv[1]
+    filt = sys.argv[2] if len(sys.argv) > 2 else ''
+    for r in kernel_resources(src):
         if filt in r['name']:
             print(f"{r['name'][:70]:70s} V={r.get('VGPRs')} S={r.get('TotalSGPRs')} Sspill={r.get('SGPRs Spill')} "
                   f"Vspill={r.get('VGPRs Spill')} scratch={r.get('ScratchSize [bytes/lane]')} occ={r.get('Occupancy [waves/SIMD]')}")
