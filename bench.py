@@ -26,9 +26,10 @@ The JSON line also carries:
   parity       -- GPU results of the timed run vs the C oracle's hash mode: every rank checks a
                   sample of its own shard; checked files and mismatches are summed over ranks.
   extras.configs -- the other BASELINE configs (3: ~600 templates, bound-pruned match
-                  kernel, plus '3-confidence': the same files through dice_batch_match_confidence
-                  (Dice#confidence: 0 without a match), and '3-allpairs': the same files on the
-                  postings kernel, which scores every pair; 4: long/mixed files; 5: full matrix + top-k) measured in the same
+                  kernel through dice_batch_match_confidence: Dice#match + #confidence, 0 for a
+                  file without a match; plus '3-top1': the same files through dice_batch_match,
+                  which also ranks the unmatched files' templates, and '3-allpairs': the same files
+                  on the postings kernel, which scores every pair; 4: long/mixed files; 5: full matrix + top-k) measured in the same
                   run (every rank, its own shard), each with its own HIP-event launch time, roofline
                   fraction, cpu_baseline and oracle parity sample.
 """
@@ -103,6 +104,16 @@ def build_workload(config: int, corpus: str = 'synthetic'):
     return TemplateCorpus(templates)
 
 
+def traffic_variant(cfg, run):
+    """The committed PMC file of a run's mode: config 3 on the postings kernels '_post', on the pruned
+    kernel through dice_batch_match '_top1'."""
+    if cfg == 3 and run.match_kernel == 3:
+        return '_post'
+    if cfg == 3 and run.match_kernel == 4 and not run.confidence:
+        return '_top1'
+    return ''
+
+
 def traffic_for(cfg, n_per, T, variant=''):
     """Per-launch HBM bytes from the committed PMC pass of this workload (variant '_post': config 3
     on the postings kernels), or None."""
@@ -149,7 +160,11 @@ class Run:
         # the file bitset as the kernels read it: tile layout (T <= 64) or row-major rows (T > 64)
         in_bytes = self.batch.bytes_per_file() if self.kind != 3 else 8 * ((self.V + 63) // 64)
         self.algo_bytes_per_file = in_bytes + 4 + 4 + 1 + out_bytes
-        self.confidence = False   # dice_batch_match_confidence ('3-confidence')
+        # dice_batch_match_confidence (Dice#match + #confidence) or dice_batch_match (also the top
+        # template of an unmatched file); --match-mode auto: the former where it changes the work
+        # (the bound-pruned kernel, config 3)
+        mode = getattr(args, 'match_mode', 'auto')
+        self.confidence = cfg != 5 and (mode == 'confidence' or (mode == 'auto' and self.match_kernel == 4))
 
     def step(self, sptr):
         if self.args.probe:
@@ -383,8 +398,7 @@ def single_file_latency(run, n_calls=400):
 def measure_extra(r, c, args, stream, sptr, cpu, group):
     steps = min(args.steps, 20)
     w, lm, ach = timed(r, steps, 2, stream, group)
-    tr, tr_src = traffic_for(c if c != '5-T600' else '5_T600', r.n_per, r.T,
-                             '_post' if (c == 3 and r.match_kernel == 3) else '')
+    tr, tr_src = traffic_for(c if c != '5-T600' else '5_T600', r.n_per, r.T, traffic_variant(c, r))
     files = r.n_per * group.world
     rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'global_files': files, 'templates': r.T,
            'vocab': r.V, 'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': files * steps / w,
@@ -393,13 +407,11 @@ def measure_extra(r, c, args, stream, sptr, cpu, group):
            'roofline_frac': ach / HBM_PEAK_GBS, 'traffic': tr, 'traffic_source': tr_src}
     if r.match_kernel == 4:
         rec['note'] = ('bound-pruned Dice#match: every (file, template) pair is decided, but only pairs whose '
-                       'overlap bound can reach the top score are scored exactly (DESIGN.md 4); scores_per_s '
-                       'counts decided pairs. 3-allpairs scores every pair')
+                       'overlap bound can reach the threshold (dice_batch_match_confidence: Dice#match + '
+                       '#confidence, dice.rb:8-14,51-53) or the top score (3-top1: dice_batch_match) are scored '
+                       'exactly (DESIGN.md 4); scores_per_s counts decided pairs. 3-allpairs scores every pair')
+        rec['entry_point'] = 'dice_batch_match_confidence' if r.confidence else 'dice_batch_match'
         rec['deferred_files'] = int(group.reduce([r.batch.deferred(sptr)], 'sum')[0])
-    if r.confidence:
-        rec['note'] = ('dice_batch_match_confidence: Dice#match + #confidence as a caller reads them (dice.rb:8-14, '
-                       '51-53); a file without a match reports 0, so the bound-pruned kernel scores only '
-                       'templates that can reach the threshold. Same files as config 3')
     if not args.no_cpu_baseline:
         n_sample = {3: 20_000, 4: 30_000, 5: 50_000, '5-T600': 10_000}[c]
         threads = cpu['threads'] if group.rank == 0 else cpu['rank_threads']
@@ -450,8 +462,10 @@ def main():
                     choices=[2, 3, 4, 5, '5-T600'])
     ap.add_argument('--files-per-gpu', type=int, default=None)
     ap.add_argument('--threshold', type=float, default=98.0)
-    ap.add_argument('--confidence', action='store_true',
-                    help='match configs: dice_batch_match_confidence (Dice#confidence, 0 without a match)')
+    ap.add_argument('--match-mode', choices=('auto', 'confidence', 'top1'), default='auto',
+                    help='match configs: dice_batch_match_confidence (Dice#match + #confidence, 0 without a '
+                         'match) or dice_batch_match (top1: also the top template of an unmatched file); auto: '
+                         'confidence on the bound-pruned kernel (config 3), top1 elsewhere')
     ap.add_argument('--topk', type=int, default=3)
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU-work budget of the baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -514,7 +528,6 @@ def main():
     cfg = args.config
     n_per = args.files_per_gpu or DEFAULT_FILES[cfg]
     run = Run(cfg, n_per, rank, world, dev, nthreads, args)
-    run.confidence = bool(args.confidence) and cfg != 5
     matrix_mode = run.cfg == 5            # configs 5 and 5-T600: full matrix + top-k
     run_T_cfg3 = cfg in (3, '5-T600')     # config 3's template corpus
     stream = torch.cuda.Stream()          # a real (non-null) stream: kernels and HIP events share it
@@ -523,8 +536,7 @@ def main():
     wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, group)
     total_files = n_per * world
     value = total_files * args.steps / wall
-    traffic, traffic_src = traffic_for(cfg if cfg != '5-T600' else '5_T600', n_per, run.T,
-                                       '_post' if (cfg == 3 and run.match_kernel == 3) else '')
+    traffic, traffic_src = traffic_for(cfg if cfg != '5-T600' else '5_T600', n_per, run.T, traffic_variant(cfg, run))
     batch, files, corpus, synth = run.batch, run.files, run.corpus, run.synth
 
     # ---- results: gathers (outside the timed region) -------------------------
@@ -702,14 +714,14 @@ def main():
             r = Run(c, args.extra_files_per_gpu or DEFAULT_FILES[c], rank, world, dev, nthreads, args)
             variants = [(str(c), None)]
             if c == 3 and r.match_kernel == 4:
-                variants += [('3-confidence', 'confidence'), ('3-allpairs', {'DICE_POST_PRUNE': '0'})]
+                variants += [('3-top1', 'top1'), ('3-allpairs', {'DICE_POST_PRUNE': '0'})]
+            conf = r.confidence
             for tag, env in variants:
-                r.confidence = env == 'confidence'
+                r.confidence = conf and env is None
                 saved = r.rescore(env, dev) if isinstance(env, dict) else None
                 extras['configs'][tag] = measure_extra(r, c, args, stream, sptr, cpu, group)
                 if saved:
                     r.restore(saved)
-            r.confidence = False
             r.close()
 
     if rank == 0:

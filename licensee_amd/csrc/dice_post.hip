@@ -51,11 +51,14 @@ namespace dice {
 #ifndef POST_DIAG
 #define POST_DIAG 0
 #endif
-// Dense partials: u8 rows ([n][tp] bytes) for files whose every prefix overlap fits a byte, u16
-// rows ([n][tp]) and a per-file flag for the others (about one config-3 file in seven: a prefix
-// of 1024 words can hold 600 of one template's). POST_PARTIALS_U8=0 writes every row as u16 (A/B).
+// Dense partials as [n][tp] u16 rows. POST_PARTIALS_U8=1 (A/B build): u8 rows ([n][tp] bytes) for
+// files whose every prefix overlap fits a byte, u16 rows and a per-file flag for the others (about
+// one config-3 file in seven: a prefix of 1024 words can hold 600 of one template's) -- half the
+// round trip's bytes, but measured slower (config 3 all pairs 4.76 vs 4.64 ms, 5-T600 6.27 vs
+// 6.16 ms, 2 interleaved reps, profiles/r4h_partials_ab.txt): the kernels are latency-bound and the
+// byte rows cost a vote pass over the stage and a flag read per tile.
 #ifndef POST_PARTIALS_U8
-#define POST_PARTIALS_U8 1
+#define POST_PARTIALS_U8 0
 #endif
 struct Partials {
     uint16_t* p16;   // [n][tp] u16 rows (files flagged 1)
@@ -878,7 +881,8 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
-// The batch's partials region: [capacity][tp] u16 rows | [capacity][tp] u8 rows | [capacity] flags.
+// The batch's partials region: [capacity][tp] u16 rows (| [capacity][tp] u8 rows | [capacity] flags
+// in a POST_PARTIALS_U8 build).
 static Partials partials_of(const dice_ctx* c, const dice_batch* b) {
     char* base = reinterpret_cast<char*>(b->d_pdense);
     const size_t n16 = (size_t)b->capacity * c->post_tp * 2, n8 = (size_t)b->capacity * c->post_tp;
@@ -899,8 +903,9 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
 }
 
 int post_reserve(dice_ctx* c, dice_batch* b) {
-    // u16 rows, u8 rows and flags (partials_of); the u16 region is only touched for flagged files
-    const size_t need = (size_t)b->capacity * c->post_tp * 3 + (size_t)b->capacity;
+    // u16 rows, and with POST_PARTIALS_U8 the u8 rows and flags (partials_of)
+    const size_t need = (size_t)b->capacity * c->post_tp * 2 +
+                        (POST_PARTIALS_U8 ? (size_t)b->capacity * c->post_tp + (size_t)b->capacity : 0);
     if (b->pdense_bytes < need) {
         if (b->d_pdense) (void)hipFree(b->d_pdense);
         b->d_pdense = nullptr;

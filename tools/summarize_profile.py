@@ -24,7 +24,7 @@ def main():
     # the product kernels of the timed region (copies/packing outside it are listed, not chosen):
     # the sparse program / dense / LDS kernels run one launch per step, the postings path two
     # (dice_post_dense + dice_post_narrow_*): a step's time and traffic sum over them
-    prefixes = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune', 'dice_defer_')
+    prefixes = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune', 'dice_defer_', 'dice_confidence')
     def base(r):
         return r['Name'].split('(')[0].replace('void ', '').replace('dice::', '')
     product = [r for r in stats if base(r).startswith(prefixes)]

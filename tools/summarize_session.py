@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PREFIXES = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune_', 'dice_defer_')
+PREFIXES = ('dice_prog_', 'dice_dense_', 'dice_lds_', 'dice_post_', 'dice_prune', 'dice_defer_', 'dice_confidence')
 
 
 def base(name):
