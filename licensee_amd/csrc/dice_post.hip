@@ -169,6 +169,34 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
     }
 }
 
+// The stage's [file][template] u16 rows of a 64-file tile out to the partials ([n][tp] u16, or
+// with POST_PARTIALS_U8 the u8 rows and flags), one file per wave at a time.
+__device__ __forceinline__ void stage_out(const uint32_t* stage32, int32_t cs, int32_t tp, int64_t f0, int64_t nn,
+                                          int wave, int nwaves, int lane, const Partials& pt) {
+    for (int fi = wave; fi < kPostFiles; fi += nwaves) {
+        const int64_t file = f0 + fi;
+        if (file >= nn) break;
+        const uint32_t* src = stage32 + (fi * cs) / 2;
+        // a byte row when every partial of the file fits a byte (one wave-wide vote), else u16
+        bool wide = !POST_PARTIALS_U8;
+        if (POST_PARTIALS_U8) {
+            bool any = false;
+            for (int32_t j = lane; j < tp / 2; j += kWave) any |= (src[j] & 0xFF00FF00u) != 0;
+            wide = __ballot(any) != 0;
+            if (lane == 0) pt.flag[file] = wide ? 1 : 0;
+        }
+        if (!wide) {
+            uint32_t* dst = pt.p8 + file * (tp / 4);
+            // bytes 0 and 2 of each u16 pair: v_perm_b32 packs four partials into one word
+            for (int32_t j = lane; j < tp / 4; j += kWave)
+                dst[j] = __builtin_amdgcn_perm(src[2 * j + 1], src[2 * j], 0x06040200u);
+        } else {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(pt.p16 + file * tp);
+            for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
+        }
+    }
+}
+
 // Phase 1 (dense prefix, lanes = files): wave w scores templates [w*TW, (w+1)*TW) over the 64
 // files' first D u64 words (DP = D rounded up to a multiple of 4; masks past D are zero). The
 // template masks are wave-uniform scalar loads, the next template's issued before this one is
@@ -258,29 +286,123 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
         for (int32_t t = T + (threadIdx.x >> 6); t < tp; t += kPostWaves) crow[t] = 0;   // row padding
     }
     __syncthreads();
-    for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
-        const int64_t file = f0 + fi;
-        if (file >= nn) break;
-        const uint32_t* src = stage32 + (fi * cs) / 2;
-        // a byte row when every partial of the file fits a byte (one wave-wide vote), else u16
-        bool wide = !POST_PARTIALS_U8;
-        if (POST_PARTIALS_U8) {
-            bool any = false;
-            for (int32_t j = lane; j < tp / 2; j += kWave) any |= (src[j] & 0xFF00FF00u) != 0;
-            wide = __ballot(any) != 0;
-            if (lane == 0) pt.flag[file] = wide ? 1 : 0;
-        }
-        if (!wide) {
-            uint32_t* dst = pt.p8 + file * (tp / 4);
-            // bytes 0 and 2 of each u16 pair: v_perm_b32 packs four partials into one word
-            for (int32_t j = lane; j < tp / 4; j += kWave)
-                dst[j] = __builtin_amdgcn_perm(src[2 * j + 1], src[2 * j], 0x06040200u);
-        } else {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(pt.p16 + file * tp);
-            for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
-        }
-    }
+    stage_out(stage32, cs, tp, f0, nn, wave, kPostWaves, lane, pt);
     __syncthreads();   // the stage is refilled by the next tile
+    }
+}
+
+// The dense prefix on the matrix cores (dice_post_dense_mfma, DICE_POST_MFMA, default 1). The
+// prefix overlap |W_F ∩ Lf_t ∩ prefix| is a binary matrix product -- files x prefix bits times
+// prefix bits x templates -- so with bits widened to int8 0/1, v_mfma_i32_32x32x32_i8 computes a
+// 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). One workgroup = 4
+// waves x 64 files (two 32-file M-tiles); wave w owns N-tiles [w NTW, (w + 1) NTW) of 32
+// templates. Per u64 prefix word q: the files' words from the LDS-staged prefixes, the
+// templates' words from dmask (L1/L2-resident, one 8-byte load per lane and N-tile), each lane's
+// 16 bits of a k-step widened to 16 bytes (nibble x 0x204081 & 0x01010101: bit i -> byte i),
+// then 2 M x NTW MFMAs per k-step. A and B place bit 16 h + j of the k-step (h = lane half) in
+// element j of their fragments: the same k on both sides, so the products pair the same bits
+// whatever the hardware's k order inside a step. The accumulators (file = row: reg & 3 +
+// 8 (reg >> 2) + 4 h, template = column: lane & 31) go to the same LDS [file][template] u16
+// stage and out as [n][tp] u16 rows (stage_out).
+constexpr int kMfmaNT = 4;   // N-tiles per wave
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ v4i widen16(uint32_t v) {
+    v4i r;
+    r.x = (int)((((v >> 0) & 0xFu) * 0x00204081u) & 0x01010101u);
+    r.y = (int)((((v >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
+    r.z = (int)((((v >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
+    r.w = (int)((((v >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
+    return r;
+}
+
+template <int DP, int NTW, int NW, int TPMAX>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void dice_post_dense_mfma(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
+    const uint64_t* __restrict__ dmask, Partials pt, const int32_t* __restrict__ idx,
+    const uint32_t* __restrict__ pn) {
+    __shared__ uint32_t stage32[kPostFiles * (TPMAX + 2) / 2];
+    uint16_t* st = reinterpret_cast<uint16_t*>(stage32);
+    const int32_t cs = tp + 2;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    constexpr int kPreStride = kPostMaxDense + 2;
+    static_assert(kPostFiles * kPreStride * 2 <= kPostFiles * (TPMAX + 2) / 2, "prefixes fit the stage");
+    const int64_t nn = idx ? (int64_t)*pn : n;
+    // this lane's template in each of the wave's N-tiles (its B column), clamped; masks of
+    // templates >= T are zero (padding partials 0)
+    const int32_t tb = wave * NTW * 32;
+    for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
+        {
+            uint64_t* pre = reinterpret_cast<uint64_t*>(stage32);
+            for (int i = threadIdx.x; i < kPostFiles * kPostMaxDense; i += NW * kWave) {
+                const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
+                const int64_t file = f0 + fi;
+                uint64_t v = 0;
+                if (file < nn && d < D) v = rows[(idx ? (int64_t)idx[file] : file) * w64 + d];
+                pre[fi * kPreStride + d] = v;
+            }
+        }
+        __syncthreads();
+        v16i acc[2][NTW];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const uint64_t* pre = reinterpret_cast<const uint64_t*>(stage32);
+        // template words of prefix word q, one 8-byte load per N-tile; word q + 1's are requested
+        // before word q's MFMAs
+        uint64_t bn[NTW];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const int32_t t = tb + j * 32 + r;
+            bn[j] = t < T ? dmask[(int64_t)t * kPostMaxDense] : 0;
+        }
+#pragma unroll 1
+        for (int q = 0; q < DP; ++q) {
+            uint64_t bw[NTW];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                bw[j] = bn[j];
+                const int32_t t = tb + j * 32 + r;
+                if (q + 1 < DP) bn[j] = t < T ? dmask[(int64_t)t * kPostMaxDense + q + 1] : 0;
+            }
+            const uint64_t a0 = pre[r * kPreStride + q], a1 = pre[(32 + r) * kPreStride + q];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int sh = 32 * ks + 16 * h;
+                const v4i fa0 = widen16((uint32_t)(a0 >> sh) & 0xFFFFu);
+                const v4i fa1 = widen16((uint32_t)(a1 >> sh) & 0xFFFFu);
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) {
+                    const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
+                    acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();   // every wave is done with the prefixes before the partials overwrite them
+        // the lane's stage addresses formed here, per tile (opaque: hoisted out of the tile loop
+        // they were 128 live VGPRs and spilled)
+        int32_t csf = cs, lf = lane;
+        asm volatile("" : "+s"(csf), "+v"(lf));
+        const int32_t rf = lf & 31, hf = lf >> 5;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const int32_t t = tb + j * 32 + rf;
+                if (t < tp) {
+                    uint16_t* col = st + (32 * m + 4 * hf) * csf + t;
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) col[((g & 3) + 8 * (g >> 2)) * csf] = (uint16_t)acc[m][j][g];
+                }
+            }
+        __syncthreads();
+        stage_out(stage32, cs, tp, f0, nn, wave, NW, lane, pt);
+        __syncthreads();   // the stage is refilled by the next tile
     }
 }
 
@@ -861,6 +983,9 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
         return fail(DICE_E_DEVICE, "postings plan upload failed");
     c->post_dense = D;
     c->post_tpad = tpad;
+    // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
+    const char* mf = getenv("DICE_POST_MFMA");
+    c->post_mfma = !(mf && *mf == '0');
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
     c->post_fast = true;
@@ -896,6 +1021,15 @@ static Partials partials_of(const dice_ctx* c, const dice_batch* b) {
 template <int DP>
 static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t groups, const int32_t* idx,
                          const uint32_t* pn) {
+    if (c->post_mfma) {
+        // 4 N-tiles of 32 templates per wave: 5 waves cover 640 templates (TPMAX 608), 6 768 (704)
+        const bool small = c->post_tp <= 608;
+        auto kern = small ? dice_post_dense_mfma<DP, kMfmaNT, 5, 608> : dice_post_dense_mfma<DP, kMfmaNT, 6, kPostMaxTpad>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3((small ? 5 : 6) * kWave), 0, s,
+                           (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
+                           (const uint64_t*)c->d_pdm, partials_of(c, b), idx, pn);
+        return;
+    }
     auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
