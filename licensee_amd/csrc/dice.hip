@@ -319,7 +319,7 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
-    void* plan[] = {c->d_lrec, c->d_lep,  c->d_les,  c->d_lwt,   c->d_pwrow, c->d_prow,  c->d_povf, c->d_pdm,
+    void* plan[] = {c->d_lrec, c->d_lep,  c->d_les,  c->d_lwt,   c->d_pdmt, c->d_prow,  c->d_povf, c->d_pdm,
                     c->d_ptc,  c->d_p4q8, c->d_p4tc, c->d_p4cc,  c->d_p4off, c->d_p4rec, c->d_p4slot};
     for (void* p : plan)
         if (p) (void)hipFree(p);
@@ -489,7 +489,7 @@ void dice_batch_destroy(dice_batch* b) {
     }
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
                     b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
-                    b->d_defer, b->d_ndefer, b->d_exact, b->d_fmask, b->d_qctr};
+                    b->d_defer, b->d_ndefer, b->d_exact, b->d_fmask};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -514,16 +514,7 @@ int dice_batch_create(dice_ctx* ctx, int64_t capacity, dice_batch** out) {
         dice_batch_destroy(b);
         return rc;
     }
-    if (ctx->kind == 1 && ctx->prog.queue) {
-        if ((rc = dalloc(&b->d_qctr, 1))) {
-            dice_batch_destroy(b);
-            return rc;
-        }
-        if (hipMemset(b->d_qctr, 0, 4) != hipSuccess) {
-            dice_batch_destroy(b);
-            return fail(DICE_E_DEVICE, "hipMemset failed");
-        }
-    }
+
     *out = b;
     return DICE_OK;
 }

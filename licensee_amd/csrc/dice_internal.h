@@ -75,7 +75,7 @@ struct dice_ctx {
     int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1, lds_wide = 0, lds_tiles = 2;
     int64_t lds_entries = 0;
     // kind 3 plan (dice_post.hip): postings rows of the narrow words, dense-prefix masks
-    void* d_pwrow = nullptr;   // (unused)
+    void* d_pdmt = nullptr;    // [16][kMfmaCols] u64 dense-prefix masks, word-major, zero-padded (MFMA kernel)
     void* d_prow = nullptr;    // [64*w64][16] u16 postings row per word (short ids / long word ref)
     void* d_povf = nullptr;    // flat u16 template ids of the long words
     void* d_pdm = nullptr;     // [T][16] u64 dense-prefix masks
@@ -175,6 +175,4 @@ struct dice_batch {
     uint64_t* d_fmask = nullptr;
     // small-call batch: d_wf/d_len/d_cc/d_rows carved from d_in, results from d_out
     void *d_in = nullptr, *d_out = nullptr;
-    // sparse program's tile queue (kind 1 with DICE_PROG_QUEUE=1): next-tile counter, 0 between launches
-    uint32_t* d_qctr = nullptr;
 };

@@ -294,17 +294,25 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // The dense prefix on the matrix cores (dice_post_dense_mfma, DICE_POST_MFMA, default 1). The
 // prefix overlap |W_F ∩ Lf_t ∩ prefix| is a binary matrix product -- files x prefix bits times
 // prefix bits x templates -- so with bits widened to int8 0/1, v_mfma_i32_32x32x32_i8 computes a
-// 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). One workgroup = 4
+// 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). One workgroup = NW
 // waves x 64 files (two 32-file M-tiles); wave w owns N-tiles [w NTW, (w + 1) NTW) of 32
-// templates. Per u64 prefix word q: the files' words from the LDS-staged prefixes, the
-// templates' words from dmask (L1/L2-resident, one 8-byte load per lane and N-tile), each lane's
-// 16 bits of a k-step widened to 16 bytes (nibble x 0x204081 & 0x01010101: bit i -> byte i),
-// then 2 M x NTW MFMAs per k-step. A and B place bit 16 h + j of the k-step (h = lane half) in
-// element j of their fragments: the same k on both sides, so the products pair the same bits
-// whatever the hardware's k order inside a step. The accumulators (file = row: reg & 3 +
-// 8 (reg >> 2) + 4 h, template = column: lane & 31) go to the same LDS [file][template] u16
-// stage and out as [n][tp] u16 rows (stage_out).
-constexpr int kMfmaNT = 4;   // N-tiles per wave
+// templates (NTW = 2: each template fragment serves both M-tiles; 64 accumulator registers,
+// 10-11 waves per workgroup at up to 3 per SIMD). Per u64 prefix word q: the files' words from
+// the LDS-staged prefixes, the templates' words from the word-major masks (staged in LDS once
+// per persistent workgroup), each lane's 16 bits of a k-step widened to 16 bytes
+// (nibble x 0x204081 & 0x01010101: bit i -> byte i), then 2 M x NTW MFMAs per k-step. A and B
+// place bit 16 h + j of the k-step (h = lane half) in element j of their fragments: the same k
+// on both sides, so the products pair the same bits whatever the hardware's k order inside a
+// step. Accumulator register g of lane (h, c) is file 32 m + (g & 3) + 8 (g >> 2) + 4 h,
+// template 32 j + c: transposed through a per-wave LDS slab and stored as 16-byte pieces of the
+// [n][tp] u16 partial rows (a wave's 64 templates of one file are 128 contiguous bytes). The next tile's prefixes are loaded into registers while this
+// tile is scored and written to the other LDS buffer after it: one barrier per tile.
+// (Measured on the way, 5-T600 dense kernel: 4 waves x 4 N-tiles through an LDS stage, one wave
+// per SIMD, 1.70 ms; with the mask ring 1.61; 10 waves x 2 N-tiles 1.31; persistent, masks in LDS,
+// next prefixes in flight, 2-byte stores 1.04; the VALU kernel 1.45.)
+constexpr int kMfmaNT = 2;       // N-tiles per wave (10 or 11 waves per workgroup)
+constexpr int kSlabStride = 72;  // u16 per slab row: rows 4 apart (the lane halves) 16 banks apart
+constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>= 11 waves x 2 N-tiles x 32)
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
@@ -317,59 +325,66 @@ __device__ __forceinline__ v4i widen16(uint32_t v) {
     return r;
 }
 
-template <int DP, int NTW, int NW, int TPMAX>
-__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void dice_post_dense_mfma(
-    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
-    const uint64_t* __restrict__ dmask, Partials pt, const int32_t* __restrict__ idx,
+template <int DP, int NTW, int NW>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
+    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
     const uint32_t* __restrict__ pn) {
-    __shared__ uint32_t stage32[kPostFiles * (TPMAX + 2) / 2];
-    uint16_t* st = reinterpret_cast<uint16_t*>(stage32);
-    const int32_t cs = tp + 2;
+    constexpr int kPreStride = kPostMaxDense + 2;   // 18 u64 per file row
+    constexpr int kPreWords = kPostFiles * kPostMaxDense;
+    constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);   // prefix words per thread
+    constexpr int kCols = NW * NTW * 32;             // the workgroup's template columns
+    __shared__ uint64_t pre[2][kPostFiles * kPreStride];
+    __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 88 KiB)
+    __shared__ uint16_t tslab[NW][32 * kSlabStride];  // per-wave transpose of one M-tile (4.5 KiB)
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
-    constexpr int kPreStride = kPostMaxDense + 2;
-    static_assert(kPostFiles * kPreStride * 2 <= kPostFiles * (TPMAX + 2) / 2, "prefixes fit the stage");
     const int64_t nn = idx ? (int64_t)*pn : n;
-    // this lane's template in each of the wave's N-tiles (its B column), clamped; masks of
-    // templates >= T are zero (padding partials 0)
     const int32_t tb = wave * NTW * 32;
-    for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
-        {
-            uint64_t* pre = reinterpret_cast<uint64_t*>(stage32);
-            for (int i = threadIdx.x; i < kPostFiles * kPostMaxDense; i += NW * kWave) {
-                const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
-                const int64_t file = f0 + fi;
-                uint64_t v = 0;
-                if (file < nn && d < D) v = rows[(idx ? (int64_t)idx[file] : file) * w64 + d];
-                pre[fi * kPreStride + d] = v;
-            }
+    const int64_t stride = (int64_t)gridDim.x * kPostFiles;
+    int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
+    if (f0 >= nn) return;
+    // this thread's share of a tile's prefix words (file i / 16, word i % 16)
+    auto load_pre = [&](int64_t fs, uint64_t (&pv)[kPer]) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = (int)threadIdx.x + k * NW * kWave;
+            const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
+            const int64_t file = fs + fi;
+            pv[k] = (i < kPreWords && file < nn && d < D) ? rows[(idx ? (int64_t)idx[file] : file) * w64 + d] : 0;
         }
-        __syncthreads();
+    };
+    auto store_pre = [&](int buf, const uint64_t (&pv)[kPer]) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = (int)threadIdx.x + k * NW * kWave;
+            if (i < kPreWords) pre[buf][(i / kPostMaxDense) * kPreStride + i % kPostMaxDense] = pv[k];
+        }
+    };
+    // the masks once per (persistent) workgroup: LDS reads in the k-loop wait on lgkmcnt, so the
+    // next tile's prefix loads (vmcnt) fly across the whole tile
+    for (int i = threadIdx.x; i < DP * kCols; i += NW * kWave) bm[i] = dmask[(i / kCols) * kMfmaCols + i % kCols];
+    uint64_t pv[kPer];
+    load_pre(f0, pv);
+    store_pre(0, pv);
+    __syncthreads();
+    for (int buf = 0; f0 < nn; f0 += stride, buf ^= 1) {
+        const bool more = f0 + stride < nn;   // uniform
+        if (more) load_pre(f0 + stride, pv);
         v16i acc[2][NTW];
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
             for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        const uint64_t* pre = reinterpret_cast<const uint64_t*>(stage32);
-        // template words of prefix word q, one 8-byte load per N-tile; word q + 1's are requested
-        // before word q's MFMAs
-        uint64_t bn[NTW];
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-            const int32_t t = tb + j * 32 + r;
-            bn[j] = t < T ? dmask[(int64_t)t * kPostMaxDense] : 0;
-        }
-#pragma unroll 1
+        const uint64_t* pb = pre[buf];
+        const uint64_t* bcol = bm + tb + r;
+#pragma unroll 2
         for (int q = 0; q < DP; ++q) {
             uint64_t bw[NTW];
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) {
-                bw[j] = bn[j];
-                const int32_t t = tb + j * 32 + r;
-                if (q + 1 < DP) bn[j] = t < T ? dmask[(int64_t)t * kPostMaxDense + q + 1] : 0;
-            }
-            const uint64_t a0 = pre[r * kPreStride + q], a1 = pre[(32 + r) * kPreStride + q];
+            for (int j = 0; j < NTW; ++j) bw[j] = bcol[q * kCols + j * 32];
+            const uint64_t a0 = pb[r * kPreStride + q], a1 = pb[(32 + r) * kPreStride + q];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const int sh = 32 * ks + 16 * h;
@@ -383,26 +398,33 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(2, 2
                 }
             }
         }
-        __syncthreads();   // every wave is done with the prefixes before the partials overwrite them
-        // the lane's stage addresses formed here, per tile (opaque: hoisted out of the tile loop
-        // they were 128 live VGPRs and spilled)
-        int32_t csf = cs, lf = lane;
-        asm volatile("" : "+s"(csf), "+v"(lf));
+        // the partials out through the wave's LDS slab, one M-tile at a time: the accumulators in
+        // as u16 (file row, template column), back as 16-byte row pieces, stored as whole 128-byte
+        // runs of the [n][tp] rows (2-byte stores straight from the accumulators: 1.04 ms)
+        int32_t tpf = tp, lf = lane;
+        asm volatile("" : "+s"(tpf), "+v"(lf));
         const int32_t rf = lf & 31, hf = lf >> 5;
+        uint16_t* slab = tslab[wave];
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < 2; ++m) {
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) {
-                const int32_t t = tb + j * 32 + rf;
-                if (t < tp) {
-                    uint16_t* col = st + (32 * m + 4 * hf) * csf + t;
+            for (int j = 0; j < NTW; ++j)
 #pragma unroll
-                    for (int g = 0; g < 16; ++g) col[((g & 3) + 8 * (g >> 2)) * csf] = (uint16_t)acc[m][j][g];
-                }
+                for (int g = 0; g < 16; ++g)
+                    slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + 32 * j + rf] = (uint16_t)acc[m][j][g];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = (lf >> 3) + 8 * i, piece = lf & 7;
+                const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
+                const int64_t file = f0 + 32 * m + row;
+                const int32_t t = tb + piece * 8;
+                if (t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
             }
-        __syncthreads();
-        stage_out(stage32, cs, tp, f0, nn, wave, NW, lane, pt);
-        __syncthreads();   // the stage is refilled by the next tile
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (more) store_pre(buf ^ 1, pv);
+        __syncthreads();   // the other buffer is complete; this one is free for the tile after next
     }
 }
 
@@ -976,6 +998,13 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     if ((rc = dalloc_bytes(&c->d_prow, prow.size() * 2)) || (rc = dalloc_bytes(&c->d_povf, plong.size() * 2)) ||
         (rc = dalloc_bytes(&c->d_pdm, dm.size() * 8)) || (rc = dalloc_bytes(&c->d_ptc, tcv.size() * sizeof(uint2))))
         return rc;
+    // the same masks word-major for the MFMA kernel: [q][kMfmaCols], zero for t >= T
+    std::vector<uint64_t> dmt((size_t)kPostMaxDense * kMfmaCols, 0);
+    for (int32_t i = 0; i < T; ++i)
+        for (int d = 0; d < kPostMaxDense; ++d) dmt[(size_t)d * kMfmaCols + i] = dm[(size_t)i * kPostMaxDense + d];
+    if ((rc = dalloc_bytes(&c->d_pdmt, dmt.size() * 8))) return rc;
+    if (hipMemcpy(c->d_pdmt, dmt.data(), dmt.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(DICE_E_DEVICE, "postings plan upload failed");
     if (hipMemcpy(c->d_povf, plong.data(), plong.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_prow, prow.data(), prow.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_pdm, dm.data(), dm.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1021,13 +1050,16 @@ static Partials partials_of(const dice_ctx* c, const dice_batch* b) {
 template <int DP>
 static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t groups, const int32_t* idx,
                          const uint32_t* pn) {
-    if (c->post_mfma) {
-        // 4 N-tiles of 32 templates per wave: 5 waves cover 640 templates (TPMAX 608), 6 768 (704)
-        const bool small = c->post_tp <= 608;
-        auto kern = small ? dice_post_dense_mfma<DP, kMfmaNT, 5, 608> : dice_post_dense_mfma<DP, kMfmaNT, 6, kPostMaxTpad>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3((small ? 5 : 6) * kWave), 0, s,
-                           (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
-                           (const uint64_t*)c->d_pdm, partials_of(c, b), idx, pn);
+    if (c->post_mfma && !POST_PARTIALS_U8) {
+        // kMfmaNT N-tiles of 32 templates per wave: 10 waves cover 640 templates (tp <= 640), 11 704;
+        // persistent workgroups (one per CU: 10-11 waves at 3 per SIMD), the next tile's prefixes
+        // loaded during this one
+        const bool small = c->post_tp <= 640;
+        auto kern = small ? dice_post_dense_mfma<DP, kMfmaNT, 10> : dice_post_dense_mfma<DP, kMfmaNT, 11>;
+        const int64_t g = std::min<int64_t>(groups, (int64_t)c->n_cu);
+        hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 10 : 11) * kWave), 0, s,
+                           (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->post_tp,
+                           (const uint64_t*)c->d_pdmt, partials_of(c, b).p16, idx, pn);
         return;
     }
     auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;

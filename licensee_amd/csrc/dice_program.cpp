@@ -145,27 +145,8 @@ const char* kMatchKernel = R"HIP(
 extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_match(
     const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
     const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
-    u32* __restrict__ ov_out, double* __restrict__ score_out, u32* __restrict__ qctr) {
+    u32* __restrict__ ov_out, double* __restrict__ score_out) {
     const int lane = threadIdx.x & 63;
-#if TILE_QUEUE
-    // Tile queue (a grid of resident waves): each wave takes the next tile from the batch's
-    // counter, requesting the one after it before scoring the current tile. Every wave ends with
-    // exactly one fetch past the last tile, so the launch makes n_tiles + waves fetches; the wave
-    // whose fetch is the last one resets the counter for the next launch (no memset, capturable).
-    const u32 n_tiles = (u32)((n + 63) >> 6);
-    const u32 last = n_tiles + gridDim.x * WPB - 1;
-    u32 got = 0;
-    if (lane == 0) got = atomicAdd(qctr, 1u);
-    u32 tile = __builtin_amdgcn_readfirstlane(got);
-    while (tile < n_tiles) {
-        u32 nx = 0;
-        if (lane == 0) nx = atomicAdd(qctr, 1u);
-        MATCH_TILE((i64)tile)
-        tile = __builtin_amdgcn_readfirstlane(nx);
-    }
-    if (tile == last && lane == 0) atomicExch(qctr, 0u);
-#else
-    (void)qctr;
     const i64 tile = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (tile * 64 >= n) return;
 #if WAVE_TIMING
@@ -182,7 +163,6 @@ extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_mat
         ov_out[tile * 64] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
         ov_out[tile * 64 + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
     }
-#endif
 #endif
 }
 )HIP";
@@ -395,7 +375,7 @@ static void emit_macro(std::ostringstream& s, const std::string& head, const std
 //       template is accumulated and retired in turn.
 std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool corpus_fast) {
     std::ostringstream s;
-    s << "#define WPB " << p.wpb << "\n#define TILE_QUEUE " << (p.queue ? 1 : 0) << "\n";
+    s << "#define WPB " << p.wpb << "\n";
     const char* waves = getenv("DICE_PROG_WAVES");  // optional occupancy floor (waves/SIMD) for A/B runs
     const char* order_env = getenv("DICE_PROG_ORDER");
     const char order = (order_env && *order_env == 't') ? 't' : 'd';
@@ -680,8 +660,6 @@ static std::string source_for(const dice_templates* t, Program& prog) {
     build_entries(t, w64, prog);
     const char* wpb = getenv("DICE_PROG_WPB");   // waves per workgroup (A/B runs; default 4)
     prog.wpb = wpb && *wpb ? std::max(1, std::min(16, atoi(wpb))) : 4;
-    const char* q = getenv("DICE_PROG_QUEUE");   // match kernel: tile queue over resident waves (A/B)
-    prog.queue = q && *q == '1';
     return program_source(t, prog, (w64 + 1) / 2, corpus_in_fast_envelope(t));
 }
 
@@ -703,13 +681,6 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
         if (hipMemcpy(c->d_qperm, c->prog.qperm.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
             return fail(DICE_E_DEVICE, "program tile permutation upload failed");
     }
-    if (c->prog.queue) {
-        int per_cu = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->prog_match, 64 * c->prog.wpb, 0) !=
-                hipSuccess || per_cu < 1)
-            return fail(DICE_E_DEVICE, "occupancy query for dice_prog_match failed");
-        c->prog.resident_groups = (int64_t)per_cu * c->n_cu;
-    }
     c->kind = 1;
     return DICE_OK;
 }
@@ -717,16 +688,10 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
 int program_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + 63) / 64;
     const int32_t wpb = c->prog.wpb;
-    int64_t groups = (n_tiles + wpb - 1) / wpb;
-    if (c->prog.queue) {
-        if (!b->d_qctr) return fail(DICE_E_STATE, "batch has no tile-queue counter");
-        groups = std::min(groups, c->prog.resident_groups);
-    }
-    const unsigned grid = (unsigned)groups;
+    const unsigned grid = (unsigned)((n_tiles + wpb - 1) / wpb);
     hipFunction_t fn = c->prog_match;
     int64_t n = b->n;
-    void* args[] = {&b->d_tiles, &n,        &b->d_wf,    &b->d_len, &b->d_cc,
-                    &thr,        &b->d_best, &b->d_ov, &b->d_score, &b->d_qctr};
+    void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score};
     if (hipModuleLaunchKernel(fn, grid, 1, 1, 64 * wpb, 1, 1, 0, s, args, nullptr) != hipSuccess)
         return fail(DICE_E_DEVICE, "launch dice_prog_match failed");
     return DICE_OK;

@@ -22,8 +22,6 @@ struct Program {
     std::vector<Entry> prog;          // sorted by (dword, tpl)
     std::vector<int32_t> dword_map;   // vocab dword -> file dword in the remapped layout (-1: unused)
     int32_t wpb = 4;                  // waves (64-file tiles) per workgroup
-    bool queue = false;               // match kernel: tile queue over resident waves (DICE_PROG_QUEUE)
-    int64_t resident_groups = 0;      // workgroups resident at once (queue mode's grid)
     std::vector<int32_t> qperm;       // tile slot -> vocabulary quad (empty: identity)
     size_t entries() const { return prog.size(); }
 };

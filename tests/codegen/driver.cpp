@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
         for (unsigned w = 0; w < 4; ++w) {
             const long long before = g_slow_waves;
             run_wave((unsigned)b, w, [&] {
-                dice_prog_match(tiles.data(), n, wf.data(), len.data(), cc.data(), 98.0, best.data(), ov.data(), sc_.data(), nullptr);
+                dice_prog_match(tiles.data(), n, wf.data(), len.data(), cc.data(), 98.0, best.data(), ov.data(), sc_.data());
             });
             slow_match += g_slow_waves - before;
             run_wave((unsigned)b, w, [&] {
