@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // tile is scored and written to the other LDS buffer after it: one barrier per tile.
 // (Measured on the way, 5-T600 dense kernel: 4 waves x 4 N-tiles through an LDS stage, one wave
 // per SIMD, 1.70 ms; with the mask ring 1.61; 10 waves x 2 N-tiles 1.31; persistent, masks in LDS,
-// next prefixes in flight, 2-byte stores 1.04; the VALU kernel 1.45.)
+// next prefixes in flight, 2-byte stores 1.04; LDS slabs 0.94; the VALU kernel 1.45.)
 constexpr int kMfmaNT = 2;       // N-tiles per wave (10 or 11 waves per workgroup)
 constexpr int kSlabStride = 72;  // u16 per slab row: rows 4 apart (the lane halves) 16 banks apart
 constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>= 11 waves x 2 N-tiles x 32)
