@@ -116,32 +116,6 @@ __device__ __forceinline__ bool ge(u32 oa, i32 da, u32 ob, i32 db) {
 )HIP";
 
 const char* kMatchKernel = R"HIP(
-// One 64-file tile per wave: lanes = files.
-#define MATCH_TILE(TILE)                                                                   \
-    {                                                                                      \
-    const i64 file = (TILE) * 64 + lane;                                                   \
-    const uint4* fp = files + (TILE) * (i64)(WQ * 64) + lane;                              \
-    const u32 wf = wfp[file];                                                              \
-    const i32 lf = lenp[file];                                                             \
-    const bool cc = ccp[file] != 0;                                                        \
-    FILE_PROLOGUE                                                                          \
-    const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);         \
-    /* running best: bo = template index << 24 | overlap (0xFF: none yet), bd = its denominator */ \
-    u32 bo = 0xFF000000u; i32 bd = 1;                                                      \
-    if (__all(fast)) {                                                                     \
-        MATCH_BODY(true)                                                                   \
-    } else {                                                                               \
-        MATCH_BODY(false)                                                                  \
-    }                                                                                      \
-    if (file < n) {                                                                        \
-        const i32 bi = (bo >> 24) == 0xFFu ? -1 : (i32)(bo >> 24);                         \
-        const u32 bov = bo & 0xFFFFFFu;                                                    \
-        const double s = bi >= 0 ? sc(bov, bd) : 0.0;                                      \
-        MSTORE(best_out + file, (bi >= 0 && s >= thr) ? bi : -1);                          \
-        MSTORE(ov_out + file, bov);                                                        \
-        MSTORE(score_out + file, s);                                                       \
-    }                                                                                      \
-    }
 extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_match(
     const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
     const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
@@ -149,10 +123,31 @@ extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_mat
     const int lane = threadIdx.x & 63;
     const i64 tile = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (tile * 64 >= n) return;
+    const i64 file = tile * 64 + lane;
+    const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
 #if WAVE_TIMING
     const u64 t0_ = __builtin_amdgcn_s_memrealtime();
 #endif
-    MATCH_TILE(tile)
+    const u32 wf = wfp[file];
+    const i32 lf = lenp[file];
+    const bool cc = ccp[file] != 0;
+    FILE_PROLOGUE
+    const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
+    // running best: bo = template index << 24 | overlap (0xFF: none yet), bd = its denominator
+    u32 bo = 0xFF000000u; i32 bd = 1;
+    if (__all(fast)) {
+        MATCH_BODY(true)
+    } else {
+        MATCH_BODY(false)
+    }
+    if (file < n) {
+        const i32 bi = (bo >> 24) == 0xFFu ? -1 : (i32)(bo >> 24);
+        const u32 bov = bo & 0xFFFFFFu;
+        const double s = bi >= 0 ? sc(bov, bd) : 0.0;
+        MSTORE(best_out + file, (bi >= 0 && s >= thr) ? bi : -1);
+        MSTORE(ov_out + file, bov);
+        MSTORE(score_out + file, s);
+    }
 #if WAVE_TIMING
     // diagnostics (DICE_PROG_DIAG=timing, results wrong): per wave its start and end real-time (100 MHz)
     // clock and the raw HW_ID / XCC_ID registers, in the tile's first output slots
