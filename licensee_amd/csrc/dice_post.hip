@@ -325,6 +325,35 @@ __device__ __forceinline__ v4i widen16(uint32_t v) {
     return r;
 }
 
+// A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one M-tile at
+// a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as whole
+// 128-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94).
+template <int NTW>
+__device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[2][NTW], uint16_t* slab, uint16_t* __restrict__ part,
+                                                int64_t f0, int64_t nn, int32_t tb, int32_t tp, int lane) {
+    int32_t tpf = tp, lf = lane;
+    asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
+    const int32_t rf = lf & 31, hf = lf >> 5;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int g = 0; g < 16; ++g)
+                slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + 32 * j + rf] = (uint16_t)acc[m][j][g];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = (lf >> 3) + 8 * i, piece = lf & 7;
+            const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
+            const int64_t file = f0 + 32 * m + row;
+            const int32_t t = tb + piece * 8;
+            if (t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <int DP, int NTW, int NW>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
@@ -398,33 +427,117 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
                 }
             }
         }
-        // the partials out through the wave's LDS slab, one M-tile at a time: the accumulators in
-        // as u16 (file row, template column), back as 16-byte row pieces, stored as whole 128-byte
-        // runs of the [n][tp] rows (2-byte stores straight from the accumulators: 1.04 ms)
-        int32_t tpf = tp, lf = lane;
-        asm volatile("" : "+s"(tpf), "+v"(lf));
-        const int32_t rf = lf & 31, hf = lf >> 5;
-        uint16_t* slab = tslab[wave];
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-#pragma unroll
-            for (int j = 0; j < NTW; ++j)
-#pragma unroll
-                for (int g = 0; g < 16; ++g)
-                    slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + 32 * j + rf] = (uint16_t)acc[m][j][g];
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = (lf >> 3) + 8 * i, piece = lf & 7;
-                const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
-                const int64_t file = f0 + 32 * m + row;
-                const int32_t t = tb + piece * 8;
-                if (t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
+        mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tp, lane);
         if (more) store_pre(buf ^ 1, pv);
         __syncthreads();   // the other buffer is complete; this one is free for the tile after next
+    }
+}
+
+// WA variant (T <= 640): the file fragments widened once per tile instead of by every wave. The
+// tile's raw prefix words stay in registers (each thread owns words i and i + NW*64 of the 64 x 16),
+// and chunks of 4 words are widened by their owners into one of two LDS chunk buffers
+// ([word][k-step][lane half][file] of 16 bytes: ds_read_b128 per fragment, consecutive lanes
+// consecutive files) while the waves run the previous chunk's MFMAs; a barrier per chunk.
+constexpr int kChunkQ = 4;
+template <int DP, int NTW, int NW>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma_wa(
+    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
+    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
+    const uint32_t* __restrict__ pn) {
+    constexpr int kPreWords = kPostFiles * kPostMaxDense;
+    constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);
+    constexpr int kCols = NW * NTW * 32;
+    constexpr int kNC = (DP + kChunkQ - 1) / kChunkQ;   // chunks per tile
+    constexpr int kChunkFrags = kChunkQ * 2 * 2 * kPostFiles;   // 16-byte fragments per chunk
+    __shared__ uint64_t bm[DP * kCols];
+    __shared__ uint16_t tslab[NW][32 * kSlabStride];
+    __shared__ uint4 xa[2][kChunkFrags];                 // 2 x 16 KiB
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t nn = idx ? (int64_t)*pn : n;
+    const int32_t tb = wave * NTW * 32;
+    const int64_t stride = (int64_t)gridDim.x * kPostFiles;
+    int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
+    if (f0 >= nn) return;
+    auto load_pre = [&](int64_t fs, uint64_t (&pv)[kPer]) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = (int)threadIdx.x + k * NW * kWave;
+            const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
+            const int64_t file = fs + fi;
+            pv[k] = (i < kPreWords && file < nn && d < D) ? rows[(idx ? (int64_t)idx[file] : file) * w64 + d] : 0;
+        }
+    };
+    // the owned words of chunk c, widened into buffer b: word (file, d), d = 4 c + ql
+    auto widen_chunk = [&](int c, int b, const uint64_t (&cw)[kPer]) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = (int)threadIdx.x + k * NW * kWave;
+            const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
+            if (i < kPreWords && d / kChunkQ == c) {
+                const int ql = d % kChunkQ;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const v4i w = widen16((uint32_t)(cw[k] >> (32 * ks + 16 * hh)) & 0xFFFFu);
+                        xa[b][((ql * 2 + ks) * 2 + hh) * kPostFiles + fi] =
+                            make_uint4((uint32_t)w.x, (uint32_t)w.y, (uint32_t)w.z, (uint32_t)w.w);
+                    }
+            }
+        }
+    };
+    for (int i = threadIdx.x; i < DP * kCols; i += NW * kWave) bm[i] = dmask[(i / kCols) * kMfmaCols + i % kCols];
+    uint64_t cw[kPer], pv[kPer];
+    load_pre(f0, cw);
+    widen_chunk(0, 0, cw);
+    __syncthreads();
+    for (; f0 < nn; f0 += stride) {
+        const bool more = f0 + stride < nn;   // uniform
+        if (more) load_pre(f0 + stride, pv);
+        v16i acc[2][NTW];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const uint64_t* bcol = bm + tb + r;
+#pragma unroll 1
+        for (int c = 0; c < kNC; ++c) {
+            if (c + 1 < kNC) widen_chunk(c + 1, (c + 1) & 1, cw);
+            const uint4* xb = xa[c & 1];
+#pragma unroll
+            for (int ql = 0; ql < kChunkQ; ++ql) {
+                const int q = c * kChunkQ + ql;
+                if (q < DP) {
+                    uint64_t bw[NTW];
+#pragma unroll
+                    for (int j = 0; j < NTW; ++j) bw[j] = bcol[q * kCols + j * 32];
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks) {
+                        const uint4 u0 = xb[((ql * 2 + ks) * 2 + h) * kPostFiles + r];
+                        const uint4 u1 = xb[((ql * 2 + ks) * 2 + h) * kPostFiles + 32 + r];
+                        const v4i fa0 = v4i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w};
+                        const v4i fa1 = v4i{(int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
+                        const int sh = 32 * ks + 16 * h;
+#pragma unroll
+                        for (int j = 0; j < NTW; ++j) {
+                            const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
+                            acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
+                            acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+            __syncthreads();   // chunk c + 1 widened; chunk c's buffer free
+        }
+        mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tp, lane);
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) cw[k] = pv[k];
+            widen_chunk(0, 0, cw);   // buffer 0 was last read by chunk kNC - 2 (kNC even) or before a barrier
+        }
+        __syncthreads();
     }
 }
 
@@ -1015,6 +1128,8 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
     const char* mf = getenv("DICE_POST_MFMA");
     c->post_mfma = !(mf && *mf == '0');
+    const char* wa = getenv("DICE_POST_MFMA_WA");   // file fragments widened once per tile (T <= 640)
+    c->post_mfma_wa = !(wa && *wa == '0');
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
     c->post_fast = true;
@@ -1055,7 +1170,8 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
         // persistent workgroups (one per CU: 10-11 waves at 3 per SIMD), the next tile's prefixes
         // loaded during this one
         const bool small = c->post_tp <= 640;
-        auto kern = small ? dice_post_dense_mfma<DP, kMfmaNT, 10> : dice_post_dense_mfma<DP, kMfmaNT, 11>;
+        auto kern = small ? (c->post_mfma_wa ? dice_post_dense_mfma_wa<DP, kMfmaNT, 10> : dice_post_dense_mfma<DP, kMfmaNT, 10>)
+                          : dice_post_dense_mfma<DP, kMfmaNT, 11>;
         const int64_t g = std::min<int64_t>(groups, (int64_t)c->n_cu);
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 10 : 11) * kWave), 0, s,
                            (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->post_tp,
