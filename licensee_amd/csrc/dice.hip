@@ -651,7 +651,9 @@ static int batch_match(dice_batch* b, double thr, void* stream, bool confidence)
         int rc = dice::lds_launch_match(c, b, thr, s);
         if (rc != DICE_OK) return rc;
     } else if (c->kind == 3) {
-        int rc = c->prune ? dice::prune_launch_match(c, b, thr, s, confidence) : dice::post_launch_match(c, b, thr, s);
+        // the T > 64 kernels write Dice#confidence outputs themselves
+        int rc = c->prune ? dice::prune_launch_match(c, b, thr, s, confidence)
+                          : dice::post_launch_match(c, b, thr, s, confidence);
         if (rc != DICE_OK) return rc;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
@@ -659,7 +661,7 @@ static int batch_match(dice_batch* b, double thr, void* stream, bool confidence)
                            b->d_ov, b->d_score);
     }
     HIP_TRY(hipGetLastError());
-    if (confidence) {
+    if (confidence && c->kind != 3) {
         hipLaunchKernelGGL(dice_confidence_outputs, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0, s, b->d_best,
                            b->d_ov, b->d_score, b->n);
         HIP_TRY(hipGetLastError());

@@ -82,7 +82,6 @@ struct dice_ctx {
     void* d_ptc = nullptr;     // [T] int4 template constants
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_ld = 0;
     bool post_fast = false;
-    bool post_mfma_wa = true;  // ... with the file fragments widened once per tile (DICE_POST_MFMA_WA)
     bool post_mfma = true;     // dense prefix by dice_post_dense_mfma (DICE_POST_MFMA=0: the VALU kernel)
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --
@@ -115,11 +114,12 @@ int lds_setup(dice_ctx* c, const dice_templates* t);
 int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
 bool post_feasible(const dice_templates* t);
 int post_setup(dice_ctx* c, const dice_templates* t);
-int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s);
+// confidence: Dice#confidence outputs (overlap 0 and score 0.0 for a file without a match)
+int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bool confidence = false);
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s);
 // the deferred files idx[0 .. *pn) of a pruned match (count on the device; no host read-back)
 int post_launch_match_indexed(dice_ctx* c, dice_batch* b, double thr, const int32_t* idx, const uint32_t* pn,
-                              hipStream_t s);
+                              hipStream_t s, bool confidence = false);
 // the batch's dense-partial buffer ([capacity][tp] u16)
 int post_reserve(dice_ctx* c, dice_batch* b);
 int prune_setup(dice_ctx* c, const dice_templates* t);

@@ -297,7 +297,8 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). One workgroup = NW
 // waves x 64 files (two 32-file M-tiles); wave w owns N-tiles [w NTW, (w + 1) NTW) of 32
 // templates (NTW = 2: each template fragment serves both M-tiles; 64 accumulator registers,
-// 10-11 waves per workgroup at up to 3 per SIMD). Per u64 prefix word q: the files' words from
+// 11-12 waves per workgroup at up to 3 per SIMD, the N-tiles dealt so the SIMDs' shares differ by
+// at most one). Per u64 prefix word q: the files' words from
 // the LDS-staged prefixes, the templates' words from the word-major masks (staged in LDS once
 // per persistent workgroup), each lane's 16 bits of a k-step widened to 16 bytes
 // (nibble x 0x204081 & 0x01010101: bit i -> byte i), then 2 M x NTW MFMAs per k-step. A and B
@@ -330,7 +331,7 @@ __device__ __forceinline__ v4i widen16(uint32_t v) {
 // 128-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94).
 template <int NTW>
 __device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[2][NTW], uint16_t* slab, uint16_t* __restrict__ part,
-                                                int64_t f0, int64_t nn, int32_t tb, int32_t tp, int lane) {
+                                                int64_t f0, int64_t nn, int32_t tb, int32_t te, int32_t tp, int lane) {
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
     const int32_t rf = lf & 31, hf = lf >> 5;
@@ -348,7 +349,7 @@ __device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[2][NTW], uint1
             const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
             const int64_t file = f0 + 32 * m + row;
             const int32_t t = tb + piece * 8;
-            if (t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+            if (t < tpf && t < te && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     constexpr int kPreStride = kPostMaxDense + 2;   // 18 u64 per file row
     constexpr int kPreWords = kPostFiles * kPostMaxDense;
     constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);   // prefix words per thread
-    constexpr int kCols = NW * NTW * 32;             // the workgroup's template columns
+    constexpr int kCols = NTW == 2 && NW == 12 ? 640 : NW * NTW * 32;   // the workgroup's template columns
     __shared__ uint64_t pre[2][kPostFiles * kPreStride];
     __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 88 KiB)
     __shared__ uint16_t tslab[NW][32 * kSlabStride];  // per-wave transpose of one M-tile (4.5 KiB)
@@ -370,7 +371,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int64_t nn = idx ? (int64_t)*pn : n;
-    const int32_t tb = wave * NTW * 32;
+    // the wave's N-tiles: the ceil(tp / 32) tiles dealt as evenly as the waves allow (wave w on SIMD
+    // w mod 4: 19 tiles over 12 waves give the SIMDs 5, 5, 5, 4)
+    const int32_t ntiles = (tp + 31) / 32, tbase = ntiles / NW, textra = ntiles % NW;
+    const int32_t nw_tiles = tbase + (wave < textra ? 1 : 0);
+    const int32_t tb = 32 * (wave * tbase + min(wave, textra));
     const int64_t stride = (int64_t)gridDim.x * kPostFiles;
     int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
     if (f0 >= nn) return;
@@ -421,123 +426,17 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
                 const v4i fa1 = widen16((uint32_t)(a1 >> sh) & 0xFFFFu);
 #pragma unroll
                 for (int j = 0; j < NTW; ++j) {
-                    const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
-                    acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
-                    acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
+                    if (j < nw_tiles) {   // uniform
+                        const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
+                        acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
+                    }
                 }
             }
         }
-        mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tp, lane);
+        mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
         if (more) store_pre(buf ^ 1, pv);
         __syncthreads();   // the other buffer is complete; this one is free for the tile after next
-    }
-}
-
-// WA variant (T <= 640): the file fragments widened once per tile instead of by every wave. The
-// tile's raw prefix words stay in registers (each thread owns words i and i + NW*64 of the 64 x 16),
-// and chunks of 4 words are widened by their owners into one of two LDS chunk buffers
-// ([word][k-step][lane half][file] of 16 bytes: ds_read_b128 per fragment, consecutive lanes
-// consecutive files) while the waves run the previous chunk's MFMAs; a barrier per chunk.
-constexpr int kChunkQ = 4;
-template <int DP, int NTW, int NW>
-__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma_wa(
-    const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
-    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
-    const uint32_t* __restrict__ pn) {
-    constexpr int kPreWords = kPostFiles * kPostMaxDense;
-    constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);
-    constexpr int kCols = NW * NTW * 32;
-    constexpr int kNC = (DP + kChunkQ - 1) / kChunkQ;   // chunks per tile
-    constexpr int kChunkFrags = kChunkQ * 2 * 2 * kPostFiles;   // 16-byte fragments per chunk
-    __shared__ uint64_t bm[DP * kCols];
-    __shared__ uint16_t tslab[NW][32 * kSlabStride];
-    __shared__ uint4 xa[2][kChunkFrags];                 // 2 x 16 KiB
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = (int)rfl(threadIdx.x >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t nn = idx ? (int64_t)*pn : n;
-    const int32_t tb = wave * NTW * 32;
-    const int64_t stride = (int64_t)gridDim.x * kPostFiles;
-    int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
-    if (f0 >= nn) return;
-    auto load_pre = [&](int64_t fs, uint64_t (&pv)[kPer]) {
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = (int)threadIdx.x + k * NW * kWave;
-            const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
-            const int64_t file = fs + fi;
-            pv[k] = (i < kPreWords && file < nn && d < D) ? rows[(idx ? (int64_t)idx[file] : file) * w64 + d] : 0;
-        }
-    };
-    // the owned words of chunk c, widened into buffer b: word (file, d), d = 4 c + ql
-    auto widen_chunk = [&](int c, int b, const uint64_t (&cw)[kPer]) {
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = (int)threadIdx.x + k * NW * kWave;
-            const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
-            if (i < kPreWords && d / kChunkQ == c) {
-                const int ql = d % kChunkQ;
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const v4i w = widen16((uint32_t)(cw[k] >> (32 * ks + 16 * hh)) & 0xFFFFu);
-                        xa[b][((ql * 2 + ks) * 2 + hh) * kPostFiles + fi] =
-                            make_uint4((uint32_t)w.x, (uint32_t)w.y, (uint32_t)w.z, (uint32_t)w.w);
-                    }
-            }
-        }
-    };
-    for (int i = threadIdx.x; i < DP * kCols; i += NW * kWave) bm[i] = dmask[(i / kCols) * kMfmaCols + i % kCols];
-    uint64_t cw[kPer], pv[kPer];
-    load_pre(f0, cw);
-    widen_chunk(0, 0, cw);
-    __syncthreads();
-    for (; f0 < nn; f0 += stride) {
-        const bool more = f0 + stride < nn;   // uniform
-        if (more) load_pre(f0 + stride, pv);
-        v16i acc[2][NTW];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        const uint64_t* bcol = bm + tb + r;
-#pragma unroll 1
-        for (int c = 0; c < kNC; ++c) {
-            if (c + 1 < kNC) widen_chunk(c + 1, (c + 1) & 1, cw);
-            const uint4* xb = xa[c & 1];
-#pragma unroll
-            for (int ql = 0; ql < kChunkQ; ++ql) {
-                const int q = c * kChunkQ + ql;
-                if (q < DP) {
-                    uint64_t bw[NTW];
-#pragma unroll
-                    for (int j = 0; j < NTW; ++j) bw[j] = bcol[q * kCols + j * 32];
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks) {
-                        const uint4 u0 = xb[((ql * 2 + ks) * 2 + h) * kPostFiles + r];
-                        const uint4 u1 = xb[((ql * 2 + ks) * 2 + h) * kPostFiles + 32 + r];
-                        const v4i fa0 = v4i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w};
-                        const v4i fa1 = v4i{(int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
-                        const int sh = 32 * ks + 16 * h;
-#pragma unroll
-                        for (int j = 0; j < NTW; ++j) {
-                            const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
-                            acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
-                            acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
-                        }
-                    }
-                }
-            }
-            __syncthreads();   // chunk c + 1 widened; chunk c's buffer free
-        }
-        mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tp, lane);
-        if (more) {
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) cw[k] = pv[k];
-            widen_chunk(0, 0, cw);   // buffer 0 was last read by chunk kNC - 2 (kNC even) or before a barrier
-        }
-        __syncthreads();
     }
 }
 
@@ -815,9 +714,11 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
         WAVE_BEST<FAST>(bi, bo, bd);
         if (lane == 0) {
             const double s = bi >= 0 ? dice_score(bo, bd) : 0.0;
-            best_out[file] = (bi >= 0 && s >= thr) ? bi : -1;
-            ov_out[file] = bo;
-            score_out[file] = s;
+            const bool hit = bi >= 0 && s >= thr;
+            // match mode k = 1: Dice#confidence outputs (0 / 0.0 for a file without a match)
+            best_out[file] = hit ? bi : -1;
+            ov_out[file] = (k == 1 && !hit) ? 0u : bo;
+            score_out[file] = (k == 1 && !hit) ? 0.0 : s;
         }
     } else if (tki) {
         uint32_t taken = 0;   // bit j: template lane + 64 j already ranked
@@ -1128,8 +1029,6 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
     const char* mf = getenv("DICE_POST_MFMA");
     c->post_mfma = !(mf && *mf == '0');
-    const char* wa = getenv("DICE_POST_MFMA_WA");   // file fragments widened once per tile (T <= 640)
-    c->post_mfma_wa = !(wa && *wa == '0');
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
     c->post_fast = true;
@@ -1170,10 +1069,9 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
         // persistent workgroups (one per CU: 10-11 waves at 3 per SIMD), the next tile's prefixes
         // loaded during this one
         const bool small = c->post_tp <= 640;
-        auto kern = small ? (c->post_mfma_wa ? dice_post_dense_mfma_wa<DP, kMfmaNT, 10> : dice_post_dense_mfma<DP, kMfmaNT, 10>)
-                          : dice_post_dense_mfma<DP, kMfmaNT, 11>;
+        auto kern = small ? dice_post_dense_mfma<DP, kMfmaNT, 12> : dice_post_dense_mfma<DP, kMfmaNT, 11>;
         const int64_t g = std::min<int64_t>(groups, (int64_t)c->n_cu);
-        hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 10 : 11) * kWave), 0, s,
+        hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 12 : 11) * kWave), 0, s,
                            (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->post_tp,
                            (const uint64_t*)c->d_pdmt, partials_of(c, b).p16, idx, pn);
         return;
@@ -1237,13 +1135,14 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_post kernels launch failed");
 }
 
-int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    return launch<false, 1>(c, b, thr, 0, s);
+// confidence: Dice#confidence outputs (the match kernel's k argument, unused in match mode, = 1)
+int post_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bool confidence) {
+    return launch<false, 1>(c, b, thr, confidence ? 1 : 0, s);
 }
 
 int post_launch_match_indexed(dice_ctx* c, dice_batch* b, double thr, const int32_t* idx, const uint32_t* pn,
-                              hipStream_t s) {
-    return launch<false, 1>(c, b, thr, 0, s, idx, pn);
+                              hipStream_t s, bool confidence) {
+    return launch<false, 1>(c, b, thr, confidence ? 1 : 0, s, idx, pn);
 }
 
 int post_launch_matrix(dice_ctx* c, dice_batch* b, int32_t k, hipStream_t s) {

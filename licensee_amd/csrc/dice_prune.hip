@@ -285,7 +285,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
     int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast,
     bool zero_base, uint32_t wf_noclamp, int32_t* __restrict__ defer, uint32_t* __restrict__ ndefer,
-    int32_t max_evals, int32_t route_cands, float llo0, uint64_t* __restrict__ diag_out) {
+    int32_t max_evals, int32_t route_cands, float llo0, bool conf, uint64_t* __restrict__ diag_out) {
     constexpr int kTP = TJ * kWave;
     // route_cands packs the routing point: candidates | exact scores before the test << 16 (0: 2)
     const int32_t route_at = (route_cands >> 16) ? (route_cands >> 16) : 2;
@@ -474,9 +474,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
             const bool mine = lane <= slot;
             if (mine && ri >= -1) {
                 const double s = ri >= 0 ? dice_score(ro, rd) : 0.0;
-                best_out[f] = (ri >= 0 && s >= thr) ? ri : -1;
-                ov_out[f] = ro;
-                score_out[f] = s;
+                const bool hit = ri >= 0 && s >= thr;
+                best_out[f] = hit ? ri : -1;
+                // confidence mode: Dice#confidence outputs, 0 / 0.0 without a match
+                ov_out[f] = (conf && !hit) ? 0u : ro;
+                score_out[f] = (conf && !hit) ? 0.0 : s;
             }
             const uint64_t dm = __ballot(mine && ri == -3);
             if (dm) {
@@ -644,7 +646,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
 }
 
 template <int J, int TJ>
-static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0) {
+static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0, bool conf) {
     constexpr int NW = kPruneWaves;
     const size_t lds = prune_lds_bytes(NW, c->w64, c->T);
     auto kern = dice_prune4<J, TJ, NW>;
@@ -678,7 +680,7 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, f
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows, b->n,
                        per_wave, c->w64, c->T, pa, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score,
                        c->post_fast, c->prune_zero_base, c->prune_wf_noclamp, b->d_defer, b->d_ndefer, max_evals,
-                       route, llo0, diag);
+                       route, llo0, conf, diag);
     if ((PRUNE_DIAG & 8) && diag) {
         // diagnostic build only: per-phase shader-clock totals over all waves, per file
         std::vector<uint64_t> h((size_t)groups * NW * (kTPhases + 1));
@@ -695,14 +697,14 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, f
 }
 
 template <int J>
-static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0) {
+static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0, bool conf) {
     switch (prune_tj(c->T)) {
-        case 2: return launch_prune<J, 2>(c, b, thr, s, llo0);
-        case 4: return launch_prune<J, 4>(c, b, thr, s, llo0);
-        case 6: return launch_prune<J, 6>(c, b, thr, s, llo0);
-        case 8: return launch_prune<J, 8>(c, b, thr, s, llo0);
-        case 10: return launch_prune<J, 10>(c, b, thr, s, llo0);
-        default: return launch_prune<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s, llo0);
+        case 2: return launch_prune<J, 2>(c, b, thr, s, llo0, conf);
+        case 4: return launch_prune<J, 4>(c, b, thr, s, llo0, conf);
+        case 6: return launch_prune<J, 6>(c, b, thr, s, llo0, conf);
+        case 8: return launch_prune<J, 8>(c, b, thr, s, llo0, conf);
+        case 10: return launch_prune<J, 10>(c, b, thr, s, llo0, conf);
+        default: return launch_prune<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s, llo0, conf);
     }
 }
 
@@ -731,16 +733,16 @@ int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bo
     if (hipMemsetAsync(b->d_ndefer, 0, 4, s) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
     const float llo0 = confidence && thr > 0 ? (float)(thr / 400.0 * (1.0 - 1.0 / 2048)) : -1.0f;
     switch ((c->w64 + kWave - 1) / kWave) {
-        case 1: rc = launch_prune_j<1>(c, b, thr, s, llo0); break;
-        case 2: rc = launch_prune_j<2>(c, b, thr, s, llo0); break;
+        case 1: rc = launch_prune_j<1>(c, b, thr, s, llo0, confidence); break;
+        case 2: rc = launch_prune_j<2>(c, b, thr, s, llo0, confidence); break;
         case 3:
-        case 4: rc = launch_prune_j<4>(c, b, thr, s, llo0); break;
+        case 4: rc = launch_prune_j<4>(c, b, thr, s, llo0, confidence); break;
         case 5:
-        case 6: rc = launch_prune_j<6>(c, b, thr, s, llo0); break;
-        default: rc = launch_prune_j<8>(c, b, thr, s, llo0); break;
+        case 6: rc = launch_prune_j<6>(c, b, thr, s, llo0, confidence); break;
+        default: rc = launch_prune_j<8>(c, b, thr, s, llo0, confidence); break;
     }
     if (rc) return rc;
-    return post_launch_match_indexed(c, b, thr, b->d_defer, b->d_ndefer, s);
+    return post_launch_match_indexed(c, b, thr, b->d_defer, b->d_ndefer, s, confidence);
 }
 
 }  // namespace dice
