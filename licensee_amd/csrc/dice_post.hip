@@ -539,12 +539,12 @@ __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int3
 // here, before its first word chunks, and copied in once those are requested -- instead of being
 // prefetched into registers during the previous file's scoring, where the matrix kernel cannot
 // afford them.
-template <int WCAP, bool LATE, int PJ, class Between>
+template <int WCAP, bool LATE, int PJ>
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
                                               const Partials& pt, int64_t pos, bool wide, int32_t tp, uint32_t* wq,
                                               uint2* lq,
                                               const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-                                              uint32_t* crow32, int lane, Between&& between) {
+                                              uint32_t* crow32, int lane) {
     uint32_t nq = 0;           // queued narrow words (wave-uniform)
     uint32_t nl = 0;           // queued long words (uniform)
     // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
@@ -556,10 +556,6 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
         uint32_t part[PJ];
         load_partials<PJ, true>(pt, pos, tp, wide, lane, part);
         if (pb < w64) load_chunks(row, w64, pb, lane, xs);
-        // (matrix mode: the previous file's row stores, issued after this file's first loads so
-        // that waiting for those loads does not wait for the stores -- vmcnt counts both, in order --
-        // and before the copy-in overwrites the counter row they read)
-        between();
         copy_in<PJ>(crow32, part, tp, wide, lane);
         if (pb < w64) {
             queue_chunks<WCAP>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
@@ -650,51 +646,6 @@ __device__ __forceinline__ gptr<E> uniform_ptr(E* p) {
     return (gptr<E>)(lo | (hi << 32));
 }
 
-// The matrix row of a scored file: overlap and IEEE score of every template (row-major [n][ld],
-// non-temporal). Called for file i after file i + 1's first loads are issued (post_narrow_body).
-template <int TJ>
-__device__ __forceinline__ void store_rows(const uint32_t* crow32, const uint2* tcs, int32_t T, int32_t ld, int64_t file,
-                                           uint32_t wf, int32_t lf, uint32_t* __restrict__ mov, double* __restrict__ msc,
-                                           int lane) {
-    const gptr<uint32_t> orow = uniform_ptr(mov + file * ld);
-    const gptr<double> srow = uniform_ptr(msc + file * ld);
-    uint32_t lo = (uint32_t)lane;
-    asm volatile("" : "+v"(lo));
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-        const int32_t t = (int32_t)lo + j * kWave;
-        if (t < T) {
-            const uint32_t ov = crow32[t];
-            const uint2 pc = tcs[t];
-            const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16, (int32_t)(pc.x & 0x7FFFFFFFu),
-                                     (int32_t)(pc.x >> 31));
-            const int32_t den = dice_den(c, wf, lf);
-#if POST_MATRIX_STORE == 3
-            __builtin_nontemporal_store(ov, orow + t);
-            __builtin_nontemporal_store(dice_score(ov, den), srow + t);
-#else
-            const double sc = dice_score(ov, den);
-            // diagnostics (POST_MATRIX_STORE, A/B builds only): bit 0 / 1 store overlaps / scores
-            // (a cleared bit still computes them), bit 2 plain stores instead of nontemporal
-            if ((POST_MATRIX_STORE & 1) || ov == 0xFFFFFFFFu) {
-                if (POST_MATRIX_STORE & 4) orow[t] = ov;
-                else __builtin_nontemporal_store(ov, orow + t);
-            }
-            if ((POST_MATRIX_STORE & 2) || ov == 0xFFFFFFFFu) {
-                if (POST_MATRIX_STORE & 4) srow[t] = sc;
-                else __builtin_nontemporal_store(sc, srow + t);
-            }
-#endif
-        }
-    }
-}
-
-// POST_ROWS_LATE (1): the matrix rows of file i stored after file i + 1's first loads; 0: during
-// file i's scoring (A/B)
-#ifndef POST_ROWS_LATE
-#define POST_ROWS_LATE 1
-#endif
-
 template <bool kMatrix, int TJ, bool FAST>
 __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs, int32_t T, int32_t ld, int64_t file, uint32_t wf,
                                              int32_t lf, bool cc, double thr, int32_t* __restrict__ best_out,
@@ -712,10 +663,8 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
     gptr<double> srow = nullptr;
     uint32_t lo = (uint32_t)lane;
     if (kMatrix) {
-        if (!POST_ROWS_LATE) {
-            orow = uniform_ptr(mov + file * ld);
-            srow = uniform_ptr(msc + file * ld);
-        }
+        orow = uniform_ptr(mov + file * ld);
+        srow = uniform_ptr(msc + file * ld);
         asm volatile("" : "+v"(lo));
     }
     constexpr int kUnroll = SCORE_UNROLL;
@@ -741,7 +690,7 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             } else {
                 lane_best<FAST>(crow32, tcs, t, wf, lf, cc, bi, bo, bd, ov, den);
             }
-            if (kMatrix && !POST_ROWS_LATE) {
+            if (kMatrix) {
 #if POST_MATRIX_STORE == 3
                 __builtin_nontemporal_store(ov, orow + t);
                 __builtin_nontemporal_store(dice_score(ov, den), srow + t);
@@ -869,11 +818,6 @@ __device__ __forceinline__ void post_narrow_body(
     // indexed (idx != NULL, match mode): position i is the deferred file idx[i] of a pruned match
     // (its dense partials at i, its row, scalars and results at idx[i]); persistent tiles
     const int64_t nn = idx ? (int64_t)*pn : n;
-    // matrix mode: the last scored file, whose rows are stored after the next file's first loads
-    // (POST_ROWS_LATE; -1: none pending)
-    int64_t pfile = -1;
-    uint32_t pwf = 0;
-    int32_t plf = 0;
     for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < nn; f0 += (int64_t)gridDim.x * kPostFiles) {
     if (kMatrix) asm volatile("" : "+s"(tp));   // (see Tf below)
     // the tile's file indices and scalars, lane l = tile file l, by vector loads; each file reads
@@ -928,10 +872,7 @@ __device__ __forceinline__ void post_narrow_body(
         }
         const bool cc = ((tcc >> fi) & 1u) != 0;
         file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow, plong, crow32,
-                                           lanef, [&] {
-                                               if (kMatrix && POST_ROWS_LATE && pfile >= 0)
-                                                   store_rows<kTJ>(crow32, tcs, Tf, ldf, pfile, pwf, plf, mov, msc, lanef);
-                                           });
+                                           lanef);
         // match mode: the wave's next file's partials fly while this one is scored
         if (!kMatrix && fi + kPostWaves < nt)
             load_partials<kPJ, false>(pt, pos + kPostWaves, tpf, (tov >> (fi + kPostWaves)) & 1, lane, pre);
@@ -939,14 +880,8 @@ __device__ __forceinline__ void post_narrow_body(
         if (POST_DIAG & 8) continue;
         score_file<kMatrix, KM, kTJ>(crow32, tcs, Tf, ldf, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
                                             k, mov, msc, tki, tks, lanef);
-        if (kMatrix && POST_ROWS_LATE) {
-            pfile = file;
-            pwf = wf;
-            plf = lf;
-        }
     }
     }
-    if (kMatrix && POST_ROWS_LATE && pfile >= 0) store_rows<kTJ>(crow32, tcs, T, ld, pfile, pwf, plf, mov, msc, lane);
 }
 
 // Match mode held to 64 VGPRs (8 waves per SIMD: two workgroups per CU); the matrix mode's
