@@ -57,7 +57,23 @@ def test_bench_two_ranks_on_one_gpu():
     assert line['extras']['process_group']['world_size'] == 2
     assert line['cpu_baseline'] and line['cpu_baseline']['value'] > 0
     assert line['parity']['mismatches'] == 0 and line['parity']['ranks_checked'] == 2
-    for tag in ('3', '3-allpairs', '5'):
+    for tag in ('3', '3-top1', '3-allpairs', '5'):
         rec = line['extras']['configs'][tag]
         assert rec['global_files'] == 40000 and rec['parity']['mismatches'] == 0, (tag, rec)
         assert rec['cpu_baseline']['value'] > 0
+
+
+def test_config3_traffic_file_per_entry_point():
+    """Config 3's roofline.traffic comes from the PMC file of the entry point measured: '3' through
+    dice_batch_match_confidence (pmc_config3.json), '3-top1' through dice_batch_match
+    (pmc_config3_top1.json), '3-allpairs' on the postings kernels (pmc_config3_post.json)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    from types import SimpleNamespace as R
+    assert bench.traffic_variant(3, R(match_kernel=4, confidence=True)) == ''
+    assert bench.traffic_variant(3, R(match_kernel=4, confidence=False)) == '_top1'
+    assert bench.traffic_variant(3, R(match_kernel=3, confidence=False)) == '_post'
+    assert bench.traffic_variant(2, R(match_kernel=1, confidence=False)) == ''
+    for name in ('pmc_config3.json', 'pmc_config3_top1.json', 'pmc_config3_post.json'):
+        assert os.path.exists(os.path.join(ROOT, 'profiles', name)), name
