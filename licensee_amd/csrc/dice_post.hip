@@ -355,56 +355,6 @@ __device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[2][NTW], uint1
     }
 }
 
-// The k-loop of one tile: for each prefix word q, NT template words (LDS) and two file words (LDS)
-// widened into fragments, then 2 x NT MFMAs per k-step. Software-pipelined: word q + 1's
-// fragments are widened while word q's MFMAs run (independent VALU beside the matrix pipe).
-template <int DP, int NTW, int NT, int kCols, int kPreStride>
-__device__ __forceinline__ void mfma_k_loop(v16i (&acc)[2][NTW], const uint64_t* pb, const uint64_t* bcol, int r, int h) {
-    auto widen_q = [&](int q, v4i (&fa)[2][2], v4i (&fb)[NT][2]) {
-        const uint64_t a0 = pb[r * kPreStride + q], a1 = pb[(32 + r) * kPreStride + q];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int sh = 32 * ks + 16 * h;
-            fa[0][ks] = widen16((uint32_t)(a0 >> sh) & 0xFFFFu);
-            fa[1][ks] = widen16((uint32_t)(a1 >> sh) & 0xFFFFu);
-        }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const uint64_t bw = bcol[q * kCols + j * 32];
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) fb[j][ks] = widen16((uint32_t)(bw >> (32 * ks + 16 * h)) & 0xFFFFu);
-        }
-    };
-    v4i fa[2][2], fb[NT][2];
-    widen_q(0, fa, fb);
-#pragma unroll 1
-    for (int q = 0; q < DP; ++q) {
-        v4i na[2][2], nb[NT][2];
-        widen_q(min(q + 1, DP - 1), na, nb);   // (the last word re-widens word DP - 1: not used)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][ks], fb[j][ks], acc[0][j], 0, 0, 0);
-                acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][ks], fb[j][ks], acc[1][j], 0, 0, 0);
-            }
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) fa[m][ks] = na[m][ks];
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) fb[j][ks] = nb[j][ks];
-        // interleave: each MFMA followed by a share of the next word's widening VALU
-#pragma unroll
-        for (int i = 0; i < 4 * NT; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, NT == 1 ? 24 : 14, 0);   // VALU
-        }
-    }
-}
-
 template <int DP, int NTW, int NW>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
@@ -463,9 +413,27 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         const uint64_t* pb = pre[buf];
         const uint64_t* bcol = bm + tb + r;
-        // one loop per tile count (uniform), so each is one block the scheduler can interleave
-        if (nw_tiles == NTW) mfma_k_loop<DP, NTW, NTW, kCols, kPreStride>(acc, pb, bcol, r, h);
-        else mfma_k_loop<DP, NTW, 1, kCols, kPreStride>(acc, pb, bcol, r, h);
+#pragma unroll 2
+        for (int q = 0; q < DP; ++q) {
+            uint64_t bw[NTW];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) bw[j] = bcol[q * kCols + j * 32];
+            const uint64_t a0 = pb[r * kPreStride + q], a1 = pb[(32 + r) * kPreStride + q];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int sh = 32 * ks + 16 * h;
+                const v4i fa0 = widen16((uint32_t)(a0 >> sh) & 0xFFFFu);
+                const v4i fa1 = widen16((uint32_t)(a1 >> sh) & 0xFFFFu);
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) {
+                    if (j < nw_tiles) {   // uniform
+                        const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
+                        acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
+                    }
+                }
+            }
+        }
         mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
         if (more) store_pre(buf ^ 1, pv);
         __syncthreads();   // the other buffer is complete; this one is free for the tile after next
