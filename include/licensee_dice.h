@@ -146,6 +146,10 @@ int dice_similarity_matrix(dice_ctx *ctx, const dice_files *files,
 #define DICE_GATHER_DEVICE 1
 int dice_match_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files, double threshold,
                        int32_t gather_mode, int32_t *best, uint32_t *overlap, double *score);
+/* dice_match_confidence's outputs (Dice#match + #confidence, dice.rb:8-14, 51-53), sharded. */
+int dice_match_sharded_confidence(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files,
+                                  double threshold, int32_t gather_mode, int32_t *best, uint32_t *overlap,
+                                  double *score);
 int dice_similarity_matrix_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const dice_files *files,
                                    int32_t gather_mode, uint32_t *overlap, double *score, int32_t k,
                                    int32_t *topk_index, double *topk_score);

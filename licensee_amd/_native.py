@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     'dice_match_sharded', 'dice_similarity_matrix_sharded', 'dice_batch_upload_ids', 'dice_last_gather_peer',
     'dice_batch_deferred',
     'dice_ctx_match_kernel', 'dice_exact_setup', 'dice_batch_exact', 'dice_batch_download_exact', 'dice_exact',
-    'dice_match_confidence', 'dice_batch_match_confidence',
+    'dice_match_confidence', 'dice_batch_match_confidence', 'dice_match_sharded_confidence',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -116,6 +116,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_stream_probe': (ctypes.c_int, [vp, vp]),
         'dice_last_error': (ctypes.c_char_p, []),
         'dice_match_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), ctypes.c_double, i32, vp, vp, vp]),
+        'dice_match_sharded_confidence': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), ctypes.c_double, i32, vp, vp,
+                                                         vp]),
         'dice_similarity_matrix_sharded': (ctypes.c_int, [vp, i32, ctypes.POINTER(_Files), i32, vp, vp, i32,
                                                           vp, vp]),
         'dice_last_gather_peer': (i32, []),
@@ -408,10 +410,12 @@ def _ctx_array(scorers):
     return arr, len(scorers), scorers[0].n_templates
 
 
-def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DICE_GATHER_HOST):
-    """``dice_match_sharded``: the files split into contiguous shards, one per Scorer (each on
-    its own device, host thread and stream), results gathered on the host or on the first
-    Scorer's device. Every Scorer must hold the same corpus."""
+def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DICE_GATHER_HOST,
+                  confidence: bool = False):
+    """``dice_match_sharded`` (``dice_match_sharded_confidence`` with confidence=True): the files
+    split into contiguous shards, one per Scorer (each on its own device, host thread and stream),
+    results gathered on the host or on the first Scorer's device. Every Scorer must hold the same
+    corpus."""
     arr, n_ctx, _ = _ctx_array(scorers)
     n = files.n
     best = np.empty(n, np.int32)
@@ -419,8 +423,9 @@ def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DIC
     score = np.empty(n, np.float64)
     if n:
         st = files._struct()
-        _check(load_library().dice_match_sharded(arr, n_ctx, ctypes.byref(st), float(threshold), int(gather),
-                                                 _ptr(best), _ptr(ov), _ptr(score)))
+        lib = load_library()
+        fn = lib.dice_match_sharded_confidence if confidence else lib.dice_match_sharded
+        _check(fn(arr, n_ctx, ctypes.byref(st), float(threshold), int(gather), _ptr(best), _ptr(ov), _ptr(score)))
     return best, ov, score
 
 

@@ -203,8 +203,10 @@ int gather_d2h(dice_ctx* c0, const std::vector<std::pair<void*, size_t>>& outs, 
 
 extern "C" {
 
-int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, double thr, int32_t gather,
-                       int32_t* best, uint32_t* ov, double* score) {
+}  // extern "C"
+
+static int match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, double thr, int32_t gather,
+                         int32_t* best, uint32_t* ov, double* score, bool confidence) {
     int rc = check_ctxs(ctxs, n_ctx, f, gather);
     if (rc) return rc;
     const int64_t n = f->n_files;
@@ -227,7 +229,9 @@ int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f
         int r = dice::scratch_for(c, s.hi - s.lo, &b);
         if (r) return r;
         const dice_files part = slice(f, s.lo, s.hi, w64);
-        if ((r = upload_shard(c, b, &part)) || (r = dice_batch_match(b, thr, nullptr))) return r;
+        if ((r = upload_shard(c, b, &part)) ||
+            (r = confidence ? dice_batch_match_confidence(b, thr, nullptr) : dice_batch_match(b, thr, nullptr)))
+            return r;
         if (dev)
             return dice::download_match_to(b, best ? g_best + s.lo : nullptr, ov ? g_ov + s.lo : nullptr,
                                            score ? g_score + s.lo : nullptr, c->stream, hipMemcpyDefault);
@@ -238,6 +242,18 @@ int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f
         rc = gather_d2h(ctxs[0], {{best, (size_t)n * 4}, {ov, (size_t)n * 4}, {score, (size_t)n * 8}}, dev);
     if (dev) (void)hipFree(dev);
     return rc;
+}
+
+extern "C" {
+
+int dice_match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, double thr, int32_t gather,
+                       int32_t* best, uint32_t* ov, double* score) {
+    return match_sharded(ctxs, n_ctx, f, thr, gather, best, ov, score, false);
+}
+
+int dice_match_sharded_confidence(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, double thr,
+                                  int32_t gather, int32_t* best, uint32_t* ov, double* score) {
+    return match_sharded(ctxs, n_ctx, f, thr, gather, best, ov, score, true);
 }
 
 int dice_similarity_matrix_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, int32_t gather,

@@ -1,4 +1,4 @@
-"""Multi-device Dice through the C-ABI (dice_match_sharded / dice_similarity_matrix_sharded)
+"""Multi-device Dice through the C-ABI (dice_match_sharded[_confidence] / dice_similarity_matrix_sharded)
 and the one-process-per-GPU path under torch.distributed.run.
 
 On the one-GPU box the shards' contexts share device 0 (each still has its own host thread,
@@ -100,9 +100,14 @@ def test_sharded_large_corpus_lds():
     scs = _scorers(corpus, 2)
     assert scs[0].info()[2] in (2, 3)
     ref = scs[0].match(fb, 98.0)
+    conf = scs[0].match(fb, 98.0, confidence=True)
     for gather in (0, 1):
         for a, b in zip(match_sharded(scs, fb, 98.0, gather), ref):
             assert np.array_equal(a, b)
+        # dice_match_sharded_confidence: the pruned kernel's confidence outputs, sharded
+        for a, b in zip(match_sharded(scs, fb, 98.0, gather, confidence=True), conf):
+            assert np.array_equal(a, b)
+    assert np.array_equal(conf[0], ref[0]) and np.all(conf[2][ref[0] < 0] == 0.0)
     part = _sub(fb, 3001)
     for a, b in zip(matrix_sharded(scs, part, 4, 1), scs[1].matrix(part, 4)):
         assert np.array_equal(a, b)
