@@ -300,11 +300,10 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // 11-12 waves per workgroup at up to 3 per SIMD, the N-tiles dealt so the SIMDs' shares differ by
 // at most one). Per u64 prefix word q: the files' words from
 // the LDS-staged prefixes, the templates' words from the word-major masks (staged in LDS once
-// per persistent workgroup), each lane's 16 bits of a k-step widened to 16 bytes
-// (nibble x 0x204081 & 0x01010101: bit i -> byte i), then 2 M x NTW MFMAs per k-step. A and B
-// place bit 16 h + j of the k-step (h = lane half) in element j of their fragments: the same k
-// on both sides, so the products pair the same bits whatever the hardware's k order inside a
-// step. Accumulator register g of lane (h, c) is file 32 m + (g & 3) + 8 (g >> 2) + 4 h,
+// per persistent workgroup), each lane's 16 bits of a k-step widened to 16 bytes (widen_half:
+// two VALU per dword), then 2 M x NTW MFMAs per k-step. A and B place the same bit in the same
+// fragment element, so the products pair the same bits whatever the hardware's k order inside
+// a step. Accumulator register g of lane (h, c) is file 32 m + (g & 3) + 8 (g >> 2) + 4 h,
 // template 32 j + c: transposed through a per-wave LDS slab and stored as 16-byte pieces of the
 // [n][tp] u16 partial rows (a wave's 64 templates of one file are 128 contiguous bytes). The next tile's prefixes are loaded into registers while this
 // tile is scored and written to the other LDS buffer after it: one barrier per tile.
@@ -317,12 +316,17 @@ constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>=
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ v4i widen16(uint32_t v) {
+// Bits to int8 0/1 bytes for one fragment: half h of the 32-bit value v (a u64 word's low or high
+// dword = the k-step), dword k of the fragment = (v >> (4 h + k)) & 0x01010101, i.e. bytes = bits
+// 4h+k, 4h+k+8, 4h+k+16, 4h+k+24 -- a permutation of the k order that A and B share, so every
+// product still pairs the same bit; two VALU per dword (one for the first).
+__device__ __forceinline__ v4i widen_half(uint32_t v, int h) {
+    const uint32_t x = v >> (4 * h);
     v4i r;
-    r.x = (int)((((v >> 0) & 0xFu) * 0x00204081u) & 0x01010101u);
-    r.y = (int)((((v >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
-    r.z = (int)((((v >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
-    r.w = (int)((((v >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
+    r.x = (int)(x & 0x01010101u);
+    r.y = (int)((x >> 1) & 0x01010101u);
+    r.z = (int)((x >> 2) & 0x01010101u);
+    r.w = (int)((x >> 3) & 0x01010101u);
     return r;
 }
 
@@ -421,13 +425,12 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             const uint64_t a0 = pb[r * kPreStride + q], a1 = pb[(32 + r) * kPreStride + q];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                const int sh = 32 * ks + 16 * h;
-                const v4i fa0 = widen16((uint32_t)(a0 >> sh) & 0xFFFFu);
-                const v4i fa1 = widen16((uint32_t)(a1 >> sh) & 0xFFFFu);
+                const v4i fa0 = widen_half((uint32_t)(a0 >> (32 * ks)), h);
+                const v4i fa1 = widen_half((uint32_t)(a1 >> (32 * ks)), h);
 #pragma unroll
                 for (int j = 0; j < NTW; ++j) {
                     if (j < nw_tiles) {   // uniform
-                        const v4i fb = widen16((uint32_t)(bw[j] >> sh) & 0xFFFFu);
+                        const v4i fb = widen_half((uint32_t)(bw[j] >> (32 * ks)), h);
                         acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
                         acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
                     }
