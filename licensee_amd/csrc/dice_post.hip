@@ -333,14 +333,14 @@ __device__ __forceinline__ v4i widen_half(uint32_t v, int h) {
 // A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one M-tile at
 // a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as whole
 // 128-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94).
-template <int NTW>
-__device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[2][NTW], uint16_t* slab, uint16_t* __restrict__ part,
+template <int NTW, int MT>
+__device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[MT][NTW], uint16_t* slab, uint16_t* __restrict__ part,
                                                 int64_t f0, int64_t nn, int32_t tb, int32_t te, int32_t tp, int lane) {
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
     const int32_t rf = lf & 31, hf = lf >> 5;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+    for (int m = 0; m < MT; ++m) {
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
 #pragma unroll
@@ -359,16 +359,20 @@ __device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[2][NTW], uint1
     }
 }
 
-template <int DP, int NTW, int NW>
+template <int DP, int NTW, int NW, int MT>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
     const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
     const uint32_t* __restrict__ pn) {
+    // MT 32-file M-tiles per tile; the prefix buffer is doubled when LDS allows (MT = 2), else one
+    // buffer and a second barrier per tile
+    constexpr int kTF = 32 * MT;                     // files per tile
+    constexpr int kBufs = MT == 2 ? 2 : 1;
     constexpr int kPreStride = kPostMaxDense + 2;   // 18 u64 per file row
-    constexpr int kPreWords = kPostFiles * kPostMaxDense;
+    constexpr int kPreWords = kTF * kPostMaxDense;
     constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);   // prefix words per thread
     constexpr int kCols = NTW == 2 && NW == 12 ? 640 : NW * NTW * 32;   // the workgroup's template columns
-    __shared__ uint64_t pre[2][kPostFiles * kPreStride];
+    __shared__ uint64_t pre[kBufs][kTF * kPreStride];
     __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 88 KiB)
     __shared__ uint16_t tslab[NW][32 * kSlabStride];  // per-wave transpose of one M-tile (4.5 KiB)
     const int lane = threadIdx.x & (kWave - 1);
@@ -380,8 +384,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     const int32_t ntiles = (tp + 31) / 32, tbase = ntiles / NW, textra = ntiles % NW;
     const int32_t nw_tiles = tbase + (wave < textra ? 1 : 0);
     const int32_t tb = 32 * (wave * tbase + min(wave, textra));
-    const int64_t stride = (int64_t)gridDim.x * kPostFiles;
-    int64_t f0 = (int64_t)blockIdx.x * kPostFiles;
+    const int64_t stride = (int64_t)gridDim.x * kTF;
+    int64_t f0 = (int64_t)blockIdx.x * kTF;
     if (f0 >= nn) return;
     // this thread's share of a tile's prefix words (file i / 16, word i % 16)
     auto load_pre = [&](int64_t fs, uint64_t (&pv)[kPer]) {
@@ -407,12 +411,12 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     load_pre(f0, pv);
     store_pre(0, pv);
     __syncthreads();
-    for (int buf = 0; f0 < nn; f0 += stride, buf ^= 1) {
+    for (int buf = 0; f0 < nn; f0 += stride, buf = (buf + 1) % kBufs) {
         const bool more = f0 + stride < nn;   // uniform
         if (more) load_pre(f0 + stride, pv);
-        v16i acc[2][NTW];
+        v16i acc[MT][NTW];
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         const uint64_t* pb = pre[buf];
@@ -422,24 +426,29 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             uint64_t bw[NTW];
 #pragma unroll
             for (int j = 0; j < NTW; ++j) bw[j] = bcol[q * kCols + j * 32];
-            const uint64_t a0 = pb[r * kPreStride + q], a1 = pb[(32 + r) * kPreStride + q];
+            uint64_t a[MT];
+#pragma unroll
+            for (int m = 0; m < MT; ++m) a[m] = pb[(32 * m + r) * kPreStride + q];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                const v4i fa0 = widen_half((uint32_t)(a0 >> (32 * ks)), h);
-                const v4i fa1 = widen_half((uint32_t)(a1 >> (32 * ks)), h);
+                v4i fa[MT];
+#pragma unroll
+                for (int m = 0; m < MT; ++m) fa[m] = widen_half((uint32_t)(a[m] >> (32 * ks)), h);
 #pragma unroll
                 for (int j = 0; j < NTW; ++j) {
                     if (j < nw_tiles) {   // uniform
                         const v4i fb = widen_half((uint32_t)(bw[j] >> (32 * ks)), h);
-                        acc[0][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb, acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb, acc[1][j], 0, 0, 0);
+#pragma unroll
+                        for (int m = 0; m < MT; ++m)
+                            acc[m][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m], fb, acc[m][j], 0, 0, 0);
                     }
                 }
             }
         }
-        mfma_store_tile<NTW>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
-        if (more) store_pre(buf ^ 1, pv);
-        __syncthreads();   // the other buffer is complete; this one is free for the tile after next
+        if (kBufs == 1) __syncthreads();   // every wave is done with the one prefix buffer
+        mfma_store_tile<NTW, MT>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
+        if (more) store_pre((buf + 1) % kBufs, pv);
+        __syncthreads();   // the next tile's prefixes are complete (MT = 2: the other buffer)
     }
 }
 
@@ -1032,6 +1041,8 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
     const char* mf = getenv("DICE_POST_MFMA");
     c->post_mfma = !(mf && *mf == '0');
+    const char* mt = getenv("DICE_POST_MFMA_MT");   // 32-file M-tiles per MFMA tile (2 or 3; A/B)
+    c->post_mfma_mt = (mt && *mt == '3') ? 3 : 2;
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
     c->post_fast = true;
@@ -1072,8 +1083,11 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
         // persistent workgroups (one per CU: 10-11 waves at 3 per SIMD), the next tile's prefixes
         // loaded during this one
         const bool small = c->post_tp <= 640;
-        auto kern = small ? dice_post_dense_mfma<DP, kMfmaNT, 12> : dice_post_dense_mfma<DP, kMfmaNT, 11>;
-        const int64_t g = std::min<int64_t>(groups, (int64_t)c->n_cu);
+        auto kern = small ? (c->post_mfma_mt == 3 ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3>
+                                                  : dice_post_dense_mfma<DP, kMfmaNT, 12, 2>)
+                          : dice_post_dense_mfma<DP, kMfmaNT, 11, 2>;
+        const int64_t mtiles = (b->n + 32 * c->post_mfma_mt - 1) / (32 * c->post_mfma_mt);
+        const int64_t g = std::min<int64_t>(std::min<int64_t>(groups, mtiles), (int64_t)c->n_cu);
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 12 : 11) * kWave), 0, s,
                            (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->post_tp,
                            (const uint64_t*)c->d_pdmt, partials_of(c, b).p16, idx, pn);

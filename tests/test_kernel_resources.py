@@ -44,7 +44,7 @@ def test_config3_pruned_kernel_fits_8_waves_without_scratch():
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
 def test_mfma_dense_prefix_kernel_fits_2_waves_without_scratch():
     res = _resources('dice_post.hip')
-    for name in ('dice_post_dense_mfma<16, 2, 12>', 'dice_post_dense_mfma<16, 2, 11>'):
+    for name in ('dice_post_dense_mfma<16, 2, 12, 2>', 'dice_post_dense_mfma<16, 2, 12, 3>', 'dice_post_dense_mfma<16, 2, 11, 2>'):
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0' and r['VGPRs Spill'] == '0', (name, r)
         assert int(r['Occupancy [waves/SIMD]']) >= 3, (name, r)
