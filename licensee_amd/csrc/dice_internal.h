@@ -83,7 +83,7 @@ struct dice_ctx {
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_ld = 0;
     bool post_fast = false;
     bool post_mfma = true;
-    int32_t post_mfma_mt = 2;  // 32-file M-tiles per MFMA tile (DICE_POST_MFMA_MT)     // dense prefix by dice_post_dense_mfma (DICE_POST_MFMA=0: the VALU kernel)
+    int32_t post_mfma_mt = 3;  // 32-file M-tiles per MFMA tile (T <= 640; DICE_POST_MFMA_MT=2 for A/B)     // dense prefix by dice_post_dense_mfma (DICE_POST_MFMA=0: the VALU kernel)
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --
     // group bytes, constants, CC masks, template index | record offset, records, slot bounds

@@ -1042,7 +1042,7 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     const char* mf = getenv("DICE_POST_MFMA");
     c->post_mfma = !(mf && *mf == '0');
     const char* mt = getenv("DICE_POST_MFMA_MT");   // 32-file M-tiles per MFMA tile (2 or 3; A/B)
-    c->post_mfma_mt = (mt && *mt == '3') ? 3 : 2;
+    c->post_mfma_mt = (mt && *mt == '2') ? 2 : 3;
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
     c->post_fast = true;
