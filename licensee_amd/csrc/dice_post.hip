@@ -294,23 +294,22 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // The dense prefix on the matrix cores (dice_post_dense_mfma, DICE_POST_MFMA, default 1). The
 // prefix overlap |W_F ∩ Lf_t ∩ prefix| is a binary matrix product -- files x prefix bits times
 // prefix bits x templates -- so with bits widened to int8 0/1, v_mfma_i32_32x32x32_i8 computes a
-// 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). One workgroup = NW
-// waves x 64 files (two 32-file M-tiles); wave w owns N-tiles [w NTW, (w + 1) NTW) of 32
-// templates (NTW = 2: each template fragment serves both M-tiles; 64 accumulator registers,
-// 11-12 waves per workgroup at up to 3 per SIMD, the N-tiles dealt so the SIMDs' shares differ by
-// at most one). Per u64 prefix word q: the files' words from
-// the LDS-staged prefixes, the templates' words from the word-major masks (staged in LDS once
-// per persistent workgroup), each lane's 16 bits of a k-step widened to 16 bytes (widen_half:
-// two VALU per dword), then 2 M x NTW MFMAs per k-step. A and B place the same bit in the same
-// fragment element, so the products pair the same bits whatever the hardware's k order inside
-// a step. Accumulator register g of lane (h, c) is file 32 m + (g & 3) + 8 (g >> 2) + 4 h,
-// template 32 j + c: transposed through a per-wave LDS slab and stored as 16-byte pieces of the
-// [n][tp] u16 partial rows (a wave's 64 templates of one file are 128 contiguous bytes). The next tile's prefixes are loaded into registers while this
-// tile is scored and written to the other LDS buffer after it: one barrier per tile.
-// (Measured on the way, 5-T600 dense kernel: 4 waves x 4 N-tiles through an LDS stage, one wave
-// per SIMD, 1.70 ms; with the mask ring 1.61; 10 waves x 2 N-tiles 1.31; persistent, masks in LDS,
-// next prefixes in flight, 2-byte stores 1.04; LDS slabs 0.94; the VALU kernel 1.45.)
-constexpr int kMfmaNT = 2;       // N-tiles per wave (10 or 11 waves per workgroup)
+// 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). A persistent workgroup
+// (one per CU) = NW waves over tiles of MT x 32 files (MT = 3 for T <= 640, else 2); wave w owns
+// 1-2 N-tiles of 32 templates (the ceil(T / 32) tiles dealt so the SIMDs' shares differ by at
+// most one; 12 waves at 3 per SIMD, 11 above 640 templates), and each template fragment serves
+// the MT M-tiles. Per u64 prefix word q: the files' words from the LDS-staged prefixes, the
+// templates' words from the word-major masks (staged in LDS once per workgroup), each lane's 16
+// bits of a k-step widened to 16 bytes (widen_half: two VALU per dword), then MT x NTW MFMAs per
+// k-step. A and B place the same bit in the same fragment element, so the products pair the same
+// bits whatever the hardware's k order inside a step. Accumulator register g of lane (h, c) is
+// file 32 m + (g & 3) + 8 (g >> 2) + 4 h, template 32 j + c: transposed through a per-wave LDS
+// slab and stored as 16-byte pieces of the [n][tp] u16 partial rows (a wave's 64 templates of one
+// file are 128 contiguous bytes). The next tile's prefixes are loaded into registers while this
+// tile is scored (LDS waits count lgkmcnt, so they fly across the tile) and written to LDS after
+// it. (5-T600 dense kernel, step by step: 1.70 ms -> 0.68 ms, the VALU kernel 1.45;
+// profiles/r4_mfma_dense.txt.)
+constexpr int kMfmaNT = 2;       // N-tiles per wave (at most)
 constexpr int kSlabStride = 72;  // u16 per slab row: rows 4 apart (the lane halves) 16 banks apart
 constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>= 11 waves x 2 N-tiles x 32)
 typedef int v4i __attribute__((ext_vector_type(4)));
