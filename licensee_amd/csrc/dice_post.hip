@@ -637,10 +637,6 @@ __device__ __forceinline__ bool lane_eval(const uint32_t* crow32, const uint2* t
 #ifndef POST_MATRIX_STORE
 #define POST_MATRIX_STORE 3
 #endif
-// Matrix scoring with two consecutive templates per lane (wider LDS reads and row stores; A/B)
-#ifndef POST_PAIR_SCORE
-#define POST_PAIR_SCORE 1
-#endif
 #define DICE_STR(x) #x
 #define DICE_UNROLL(n) _Pragma(DICE_STR(unroll n))
 // scoring loop unroll (A/B: 1, 2, 5, 10 within 1% for the matrix kernel; the match kernel
@@ -682,49 +678,6 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
         srow = uniform_ptr(msc + file * ld);
         asm volatile("" : "+v"(lo));
     }
-    if (kMatrix && POST_PAIR_SCORE) {
-        // two consecutive templates per lane (t = 2 lo + 128 p + e): one 8-byte counter read, one
-        // 16-byte constants read, one 8-byte overlap store and one 16-byte score store per pair
-        constexpr int TP = (TJ + 1) / 2;
-#pragma unroll
-        for (int p = 0; p < TP; ++p) {
-            const int32_t t0 = 2 * (int32_t)lo + p * 2 * kWave;
-            if (t0 < T) {
-                const uint2 ovp = *reinterpret_cast<const uint2*>(crow32 + t0);
-                const uint4 pcs = *reinterpret_cast<const uint4*>(tcs + t0);
-                const uint32_t ovs[2] = {ovp.x, ovp.y};
-                const uint2 pcv[2] = {make_uint2(pcs.x, pcs.y), make_uint2(pcs.z, pcs.w)};
-                int32_t dens[2];
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int32_t t = t0 + e;
-                    const uint2 pc = pcv[e];
-                    const int4 c = make_int4((int32_t)(pc.y & 0xFFFFu), (int32_t)pc.y >> 16,
-                                             (int32_t)(pc.x & 0x7FFFFFFFu), (int32_t)(pc.x >> 31));
-                    const uint32_t ov = ovs[e];
-                    const int32_t den = dice_den(c, wf, lf);
-                    dens[e] = den;
-                    if (t < T && !(c.w && cc)) {
-                        const bool b1 = bi < 0 || ge<FAST>(ov, den, bo, bd);
-                        const bool b2 = !b1 && (bi2 < 0 || ge<FAST>(ov, den, bo2, bd2));
-                        bi2 = b1 ? bi : b2 ? t : bi2;
-                        bo2 = b1 ? bo : b2 ? ov : bo2;
-                        bd2 = b1 ? bd : b2 ? den : bd2;
-                        bi = b1 ? t : bi;
-                        bo = b1 ? ov : bo;
-                        bd = b1 ? den : bd;
-                    }
-                }
-                // (t0 + 1 = T: the padding column gets the row's garbage; downloads strip it)
-                typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                typedef double f64x2 __attribute__((ext_vector_type(2)));
-                const u32x2 ovv = {ovs[0], ovs[1]};
-                const f64x2 scv = {dice_score(ovs[0], dens[0]), dice_score(ovs[1], max(dens[1], 1))};
-                __builtin_nontemporal_store(ovv, (gptr<u32x2>)(orow + t0));
-                __builtin_nontemporal_store(scv, (gptr<f64x2>)(srow + t0));
-            }
-        }
-    } else {
     constexpr int kUnroll = SCORE_UNROLL;
     DICE_UNROLL(kUnroll)
     for (int j = 0; j < TJ; ++j) {
@@ -768,7 +721,6 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             }
         }
     }
-    }
     if (!kMatrix) {
         WAVE_BEST<FAST>(bi, bo, bd);
         if (lane == 0) {
@@ -798,8 +750,7 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
                 break;
             }
             if (r + 1 < k && wi == bi) {   // the owner lane: next best among its untaken templates
-                // slot of template wi in its lane (pairs: 2 (t >> 7) + (t & 1))
-                taken |= 1u << (POST_PAIR_SCORE ? 2 * (wi >> 7) + (wi & 1) : (wi >> 6));
+                taken |= 1u << (wi >> 6);
                 const bool promote = POST_TOPK_SECOND && second;
                 second = false;
                 if (promote) {
@@ -810,9 +761,8 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
                     bi = -1;
                     bo = 0;
                     bd = 1;
-                    for (int j = 0; j < (POST_PAIR_SCORE ? 2 * ((TJ + 1) / 2) : TJ); ++j) {
-                        const int32_t t = POST_PAIR_SCORE ? 2 * (int32_t)lo + (j >> 1) * 2 * kWave + (j & 1)
-                                                          : (int32_t)lo + j * kWave;
+                    for (int j = 0; j < TJ; ++j) {
+                        const int32_t t = (int32_t)lo + j * kWave;
                         if (t < T && !((taken >> j) & 1u)) {
                             uint32_t ov;
                             int32_t den;
@@ -864,7 +814,7 @@ __device__ __forceinline__ void post_narrow_body(
     constexpr int kWCap = word_cap<TPMAX>();
     constexpr int kPJ = pairs_per_lane<TPMAX>();
     __shared__ uint32_t cnt32[kPostWaves * TPMAX];             // u32 counters, one row per wave
-    __shared__ __attribute__((aligned(16))) uint2 tcs[TPMAX + 2];   // packed template constants (+ pair padding)
+    __shared__ uint2 tcs[TPMAX];                               // packed template constants
     __shared__ uint32_t wq[kPostWaves][kWCap];                 // queued narrow word ids
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
     __shared__ uint2 tsc[kMatrix ? kPostWaves : 1][kPostFiles / kPostWaves];   // matrix: own files' {|W_F|, len_F}
@@ -872,7 +822,6 @@ __device__ __forceinline__ void post_narrow_body(
     const int wave = (int)rfl(threadIdx.x >> 6);
     uint32_t* crow32 = cnt32 + wave * TPMAX;
     for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
-    if (threadIdx.x < 2) tcs[T + threadIdx.x] = make_uint2(0, 0);   // a pair's second past T
     for (int i = lane; i < TPMAX; i += kWave) crow32[i] = 0;
     __syncthreads();
 
