@@ -13,11 +13,12 @@
 // (in hundreds of templates) stay bitset-scored: the vocabulary's first D u64 words (the host
 // packs the widest words first) are ANDed against dense template masks.
 //
-// Two kernels per launch, each workgroup = 16 waves over one tile of 64 files:
-//   dice_post_dense (lanes = files): wave w scores templates [w*TW, (w+1)*TW) over the files'
-//            first D u64 words (template masks wave-uniform: scalar loads) into an LDS
-//            [file][template] u16 stage, written out as a row-major [n][tp] u16 matrix
-//            (2 workgroups per CU while the stage fits twice in LDS);
+// Two kernels per launch:
+//   dice_post_dense_mfma (default): the files' first D u64 words against the template masks as a
+//            binary matrix product on the matrix cores (int8 MFMA, persistent workgroups; see
+//            below), written as a row-major [n][tp] u16 matrix; dice_post_dense (DICE_POST_MFMA=0,
+//            lanes = files, 16 waves per 64-file tile): the same by v_bcnt, template masks by
+//            scalar loads, through an LDS [file][template] u16 stage;
 //   dice_post_narrow_{match,matrix} (one file per wave): the file's dense partials, widened,
 //            start the wave's u32 counter row in LDS; its remaining u64 words are loaded
 //            kChunks x 64 at a time and their set bits (narrow words) are queued in a per-wave
