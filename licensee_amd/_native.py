@@ -71,12 +71,77 @@ def hip_runtime_path() -> Optional[str]:
     return p if os.path.exists(p) else None
 
 
-def _preload_hip_runtime():
+def elf_dynamic(path: str) -> Tuple[Optional[str], Tuple[str, ...]]:
+    """(DT_SONAME, DT_NEEDED entries) of an ELF64 little-endian shared object, read from its
+    program headers (PT_DYNAMIC, the string table's address mapped through PT_LOAD); (None, ())
+    when the file is not such an object."""
+    import struct
+    try:
+        with open(path, 'rb') as fh:
+            hdr = fh.read(64)
+            if len(hdr) < 64 or hdr[:4] != b'\x7fELF' or hdr[4] != 2 or hdr[5] != 1:
+                return None, ()
+            phoff, = struct.unpack_from('<Q', hdr, 0x20)
+            phentsize, phnum = struct.unpack_from('<HH', hdr, 0x36)
+            fh.seek(phoff)
+            ph = fh.read(phentsize * phnum)
+            loads, dyn = [], None
+            for i in range(phnum):
+                p_type, _, p_offset, p_vaddr, _, p_filesz, _, _ = struct.unpack_from('<IIQQQQQQ', ph, i * phentsize)
+                if p_type == 1:
+                    loads.append((p_vaddr, p_offset, p_filesz))
+                elif p_type == 2:
+                    dyn = (p_offset, p_filesz)
+            if dyn is None:
+                return None, ()
+            fh.seek(dyn[0])
+            raw = fh.read(dyn[1])
+            ents = [struct.unpack_from('<qQ', raw, o) for o in range(0, len(raw) - 15, 16)]
+            strtab = next((v for t, v in ents if t == 5), None)
+            if strtab is None:
+                return None, ()
+            base = next((off + strtab - va for va, off, sz in loads if va <= strtab < va + sz), None)
+            if base is None:
+                return None, ()
+
+            def string(o):
+                fh.seek(base + o)
+                s = fh.read(256)
+                return s[:s.index(b'\0')].decode('utf-8', 'replace') if b'\0' in s else None
+            soname = next((string(v) for t, v in ents if t == 14), None)
+            needed = tuple(string(v) for t, v in ents if t == 1)
+            return soname, tuple(x for x in needed if x)
+    except (OSError, struct.error, ValueError):
+        return None, ()
+
+
+def needed_hip_soname(lib_path: str) -> Optional[str]:
+    """The HIP runtime soname lib_path was linked against (libamdhip64.so.N), or None."""
+    return next((x for x in elf_dynamic(lib_path)[1] if x.startswith('libamdhip64.so')), None)
+
+
+def preload_decision(lib_path: str = LIB_PATH) -> Tuple[Optional[str], str]:
+    """(runtime file to map first or None, reason). The candidate (hip_runtime_path) is mapped only
+    when its DT_SONAME equals the soname lib_path needs: a torch built against another ROCm major
+    ships libamdhip64.so.6, which the library would not bind to -- mapping it anyway would only put
+    a second runtime beside the one the library loads (dice_create refuses that)."""
+    p = hip_runtime_path()
+    if not p:
+        return None, 'no candidate runtime'
+    want = needed_hip_soname(lib_path)
+    have = elf_dynamic(p)[0]
+    if want is None or have != want:
+        return None, f'{p} has soname {have!r}, {os.path.basename(lib_path)} needs {want!r}: not preloaded'
+    return p, f'{p} ({have})'
+
+
+def _preload_hip_runtime(lib_path: str = LIB_PATH):
     """One HIP runtime per process. liblicensee_dice.so needs libamdhip64.so.7 by soname; if the
     runtime torch uses is mapped first, the library binds to it, and torch (imported before or
     after) keeps one runtime and one device view. Loaded the other way round, /opt/rocm's copy
-    and torch's would both be mapped, and dice_create refuses that (dice_last_error names both)."""
-    p = hip_runtime_path()
+    and torch's would both be mapped, and dice_create refuses that (dice_last_error names both).
+    A candidate whose soname differs from the one the library needs is skipped (preload_decision)."""
+    p, _ = preload_decision(lib_path)
     if p:
         ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
 
@@ -90,7 +155,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise DiceError(f'{path} is missing: build it with `python -c "import __graft_entry__ as g; g.build()"`')
-    _preload_hip_runtime()
+    _preload_hip_runtime(path)
     lib = ctypes.CDLL(path)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {

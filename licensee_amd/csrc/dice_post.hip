@@ -425,7 +425,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
         for (int q = 0; q < DP; ++q) {
             uint64_t bw[NTW];
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) bw[j] = bcol[q * kCols + j * 32];
+            for (int j = 0; j < NTW; ++j) bw[j] = j < nw_tiles ? bcol[q * kCols + j * 32] : 0;   // (uniform: no read past bm)
             uint64_t a[MT];
 #pragma unroll
             for (int m = 0; m < MT; ++m) a[m] = pb[(32 * m + r) * kPreStride + q];

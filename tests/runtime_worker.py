@@ -5,6 +5,9 @@
 mode 'shared' : the loader maps the HIP runtime torch uses first (licensee_amd._native default)
 mode 'second' : LICENSEE_DICE_HIP_RUNTIME='' -- the library binds /opt/rocm's runtime, then torch
                 maps its own copy; dice_create must refuse with a clear message.
+mode 'stub'   : LICENSEE_DICE_HIP_RUNTIME (set by the test) names a runtime whose soname differs from
+                the library's (a torch built for another ROCm major): the loader must skip it, so
+                only the library's own runtime is mapped and dice_create works (no torch import).
 Prints one JSON line: the distinct libamdhip64 files mapped, dice_create's outcome, and (on a GPU,
 mode 'shared') the mismatches of a torch-stream batch match against the oracle."""
 import json
@@ -32,9 +35,14 @@ def main():
         os.environ['LICENSEE_DICE_HIP_RUNTIME'] = ''
     from licensee_amd import _native
     _native.load_library()                        # the library first, no torch yet
-    import torch                                  # torch after it
-    gpu = torch.cuda.is_available()
-    out = {'mode': mode, 'runtimes': mapped_runtimes(), 'torch_gpu': gpu}
+    if mode == 'stub':
+        gpu = None
+        out = {'mode': mode, 'runtimes': mapped_runtimes(), 'torch_gpu': gpu,
+               'decision': _native.preload_decision()[1]}
+    else:
+        import torch                              # torch after it
+        gpu = torch.cuda.is_available()
+        out = {'mode': mode, 'runtimes': mapped_runtimes(), 'torch_gpu': gpu}
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.license import License
     c = TemplateCorpus(License.all(hidden=True, pseudo=False))

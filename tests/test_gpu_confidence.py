@@ -139,3 +139,100 @@ def test_small_calls(config3, n):
         _check(sc, _oracle(c), part)
     finally:
         sc.close()
+
+
+def _equality_thresholds(orc, fb, count=20):
+    """`count` distinct exact top scores that occur in fb (the oracle's dice_match scores at
+    threshold 0), spread over their range and including the largest below 100 and one >= 98."""
+    _, _, top = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 0.0, nthreads=16, mode=1)
+    u = np.unique(top[top > 0])
+    pick = set(u[np.linspace(0, u.size - 1, count - 2).round().astype(int)].tolist())
+    hi = u[(u >= 98.0) & (u < 100.0)]
+    assert hi.size, 'no file scores in [98, 100)'
+    pick.add(float(hi[hi.size // 2]))
+    pick.add(float(u[u < 100.0].max()))
+    return top, sorted(pick)[-count:]
+
+
+def _check_equality(sc, orc, fb, top, thresholds, where):
+    """Dice#matches keeps similarity >= minimum_confidence (dice.rb:44-48): a file whose top score
+    EQUALS the threshold matches. The pruned kernels start their drop level at an f32 floor of the
+    threshold; every such file must still match, identical to the oracle."""
+    for thr in thresholds:
+        exp = _expected_bitset(orc, fb, thr)
+        eq = top == thr
+        assert eq.any() and (exp[0][eq] >= 0).all(), (where, thr)
+        got = sc.match(fb, thr, confidence=True)
+        _same(got, exp, (where, 'dice_match_confidence', thr))
+        full = sc.match(fb, thr)
+        m = exp[0] >= 0
+        assert np.array_equal(full[0], exp[0]), (where, 'dice_match', thr)
+        assert np.array_equal(full[1][m], exp[1][m]) and np.array_equal(full[2][m], exp[2][m]), (where, thr)
+        assert np.array_equal(full[2], top), (where, 'dice_match top score', thr)
+
+
+def _expected_bitset(orc, fb, thr):
+    best, ov, score = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, thr, nthreads=16,
+                                mode=1)
+    return best, np.where(best >= 0, ov, 0).astype(np.uint32), np.where(best >= 0, score, 0.0)
+
+
+@pytest.mark.parametrize('prune', ['1', '0'])
+def test_threshold_equal_to_achieved_score_T600(config3, prune, monkeypatch):
+    """20 exact scores achieved in a 20k-file config-3 sample as thresholds, on
+    the bound-pruned kernel (and the postings kernels as a control)."""
+    monkeypatch.setenv('DICE_POST_PRUNE', prune)
+    c, fb = config3
+    orc = _oracle(c)
+    top, thresholds = _equality_thresholds(orc, fb)
+    assert len(thresholds) == 20
+    sc = _scorer(c)
+    try:
+        assert sc.match_kernel() == (4 if prune == '1' else 3)
+        _check_equality(sc, orc, fb, top, thresholds, ('T600', prune))
+        b = sc.batch(fb.n)
+        try:
+            b.upload(fb)
+            for thr in thresholds[::4] + thresholds[-2:]:
+                b.match(thr, confidence=True)
+                _same(b.download_match(), _expected_bitset(orc, fb, thr), ('batch confidence', thr))
+        finally:
+            b.close()
+    finally:
+        sc.close()
+
+
+def test_threshold_equal_to_achieved_score_T47():
+    from licensee_amd.corpus import TemplateCorpus
+    from licensee_amd.license import License
+    from licensee_amd.synth import SyntheticCorpus
+    c = TemplateCorpus(License.all(hidden=True, pseudo=False))
+    fb = SyntheticCorpus(c).generate(0, 20000, seed=4747, nthreads=16)
+    orc = _oracle(c)
+    top, thresholds = _equality_thresholds(orc, fb)
+    sc = _scorer(c)
+    try:
+        assert sc.match_kernel() == 1
+        _check_equality(sc, orc, fb, top, thresholds, 'T47')
+    finally:
+        sc.close()
+
+
+def test_threshold_equality_sharded_confidence_three_contexts(config3):
+    """dice_match_sharded_confidence over 3 contexts (all on device 0 here), both gathers, at
+    thresholds equal to achieved scores."""
+    from licensee_amd._native import DICE_GATHER_DEVICE, DICE_GATHER_HOST, match_sharded
+    c, fb = config3
+    orc = _oracle(c)
+    top, thresholds = _equality_thresholds(orc, fb)
+    scs = [_scorer(c) for _ in range(3)]
+    try:
+        for i, thr in enumerate(thresholds[::3] + thresholds[-1:]):
+            gather = DICE_GATHER_DEVICE if i % 2 else DICE_GATHER_HOST
+            got = match_sharded(scs, fb, thr, gather=gather, confidence=True)
+            exp = _expected_bitset(orc, fb, thr)
+            assert (exp[0][top == thr] >= 0).all()
+            _same(got, exp, ('sharded confidence', gather, thr))
+    finally:
+        for s in scs:
+            s.close()

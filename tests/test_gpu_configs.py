@@ -137,6 +137,14 @@ def test_config3_shard(kernel, monkeypatch):
         eb, eo, es = _oracle(corpus).match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, 98.0,
                                            nthreads=16, mode=1)
         assert np.array_equal(best, eb) and np.array_equal(ov, eo) and np.array_equal(score, es)
+        # the bench's config-3 entry point (dice_batch_match_confidence: Dice#match + #confidence,
+        # dice.rb:8-14,51-53) on every file of the shard: the oracle's match with the unmatched
+        # files' overlap and score 0
+        batch.match(98.0, confidence=True)
+        cb, co, cs = batch.download_match()
+        m = eb >= 0
+        assert np.array_equal(cb, eb)
+        assert np.array_equal(co, np.where(m, eo, 0)) and np.array_equal(cs, np.where(m, es, 0.0))
     batch.close()
     # matrix/top-k on a 50k slice agrees with the match kernel's argmax
     s = _sub(fb, np.arange(50_000))

@@ -45,6 +45,25 @@ def select_kernel(monkeypatch, kernel):
 
 @pytest.mark.parametrize('n_templates,kernel', CASES)
 def test_corpus_size(n_templates, kernel, monkeypatch):
+    _check_corpus(n_templates, kernel, monkeypatch)
+
+
+# the postings kernels' dense-prefix variants: the matrix-core kernel with 3 or 2
+# 32-file M-tiles per tile (12 waves, tp <= 640) and its 11-wave form above 640 templates (672,
+# 700), and the VALU kernel (DICE_POST_MFMA=0)
+PREFIX_VARIANTS = {'mfma-mt3': {}, 'mfma-mt2': {'DICE_POST_MFMA_MT': '2'}, 'valu': {'DICE_POST_MFMA': '0'}}
+
+
+@pytest.mark.parametrize('variant', sorted(PREFIX_VARIANTS))
+@pytest.mark.parametrize('n_templates', [130, 600, 672, 700])
+def test_postings_dense_prefix_variants(n_templates, variant, monkeypatch):
+    for k, v in PREFIX_VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv('DICE_POST_PRUNE', '0')
+    _check_corpus(n_templates, 'post', monkeypatch)
+
+
+def _check_corpus(n_templates, kernel, monkeypatch):
     from licensee_amd._native import Scorer
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
