@@ -428,6 +428,144 @@ def measure_extra(r, c, args, stream, sptr, cpu, group):
     return rec
 
 
+def gather_compare(batch, group, rank, world, n_per, best, ov, score, sptr, reps=3):
+    """The one result move of a sharded run, two ways, both ending with every rank's 16-B/file
+    results in rank 0's host memory (north_star: RCCL solely for the gather, or a host gather if
+    faster), each timed end to end from a barrier (median of `reps`, max over ranks):
+      host -- each rank's D2H lands straight in its slice of a node-shared, page-locked host buffer
+              that rank 0 owns (licensee_amd.shard.SharedResults), then one barrier;
+      rccl -- results packed on the device and gathered to rank 0 over xGMI (dist.gather), then
+              one D2H into rank 0's page-locked buffer (nccl backend only: ranks on distinct
+              devices).
+    Rank 0 checks both gathers against each rank's own download."""
+    import torch
+    import torch.distributed as dist
+    from licensee_amd._native import _check, _ptr, load_library
+    from licensee_amd.shard import SharedResults, gather_packed_to0, device_results_packed, pack_results
+    lib = load_library()
+    name = f"licensee_bench_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+    shared = SharedResults(name, world, n_per, create=True) if rank == 0 else None
+    group.barrier()
+    if shared is None:
+        shared = SharedResults(name, world, n_per, create=False)
+    out = {}
+    pinned = False
+    try:
+        # page-lock this process's mapping of the segment (once, outside the timed region)
+        try:
+            rt = torch.cuda.cudart()
+            pinned = int(rt.cudaHostRegister(shared.base_ptr, shared.nbytes, 0)) == 0
+        except Exception:
+            pinned = False
+        mine = shared.slice(rank)
+
+        def host_leg():
+            _check(lib.dice_batch_download_match(batch._b, _ptr(mine[0]), _ptr(mine[1]), _ptr(mine[2]), sptr or None))
+            group.barrier()
+
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            group.barrier()
+            t0 = time.perf_counter()
+            host_leg()
+            ts.append(time.perf_counter() - t0)
+        host_s = group.reduce([float(np.median(ts))], 'max')[0]
+        out['host_gather_ms'] = host_s * 1e3
+        out['host_gather'] = {'kind': 'shared-memory host buffer owned by rank 0, each rank D2H into its slice',
+                              'pinned': bool(pinned), 'bytes': 16 * n_per * world}
+        ok_host = True
+        if rank == 0:
+            ok_host = bool(np.array_equal(shared.best[:n_per], best) and np.array_equal(shared.overlap[:n_per], ov)
+                           and np.array_equal(shared.score[:n_per], score))
+        if group.backend == 'nccl':
+            res = device_results_packed(batch)
+            host_dst = torch.empty((world * n_per, 4), dtype=torch.int32, pin_memory=True) if rank == 0 else None
+            tr = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                group.barrier()
+                t0 = time.perf_counter()
+                g = gather_packed_to0(res)
+                if rank == 0:
+                    host_dst.copy_(g)
+                torch.cuda.synchronize()
+                group.barrier()
+                tr.append(time.perf_counter() - t0)
+            rccl_s = group.reduce([float(np.median(tr))], 'max')[0]
+            out['rccl_gather_ms'] = rccl_s * 1e3
+            out['gather_winner'] = 'host' if host_s <= rccl_s else 'rccl'
+            if rank == 0:
+                ref = pack_results(shared.best, shared.overlap, shared.score)
+                out['gather_agree'] = bool(np.array_equal(host_dst.numpy(), ref))
+        else:
+            out['gather_winner'] = 'host'
+            out['gather_note'] = 'ranks share a device: no RCCL communicator, host gather only'
+        oks = group.reduce([1.0 if ok_host else 0.0], 'sum')[0]
+        if rank == 0:
+            out['host_gather_checked'] = bool(ok_host) and oks == world
+        # every rank checks its own slice of the shared buffer too
+        mism = int(np.sum(mine[0] != best) + np.sum(mine[1] != ov) + np.sum(mine[2] != score))
+        out['host_gather_mismatches'] = int(group.reduce([mism], 'sum')[0])
+        group.barrier()
+    finally:
+        if pinned:
+            try:
+                torch.cuda.cudart().cudaHostUnregister(shared.base_ptr)
+            except Exception:
+                pass
+        group.barrier()
+        shared.close()
+    return out
+
+
+def abi_sharded_leg(run, args, n_dev, reps=3):
+    """The drop-in's own multi-device path in ONE process (what a Ruby/FFI caller would use,
+    INTEGRATION.md 3): dice_match_sharded_confidence over `contexts` scorers -- one per visible
+    device, or several on one device when there are fewer -- with the results gathered into the
+    caller's host buffers directly (DICE_GATHER_HOST) or through the first device (DICE_GATHER_DEVICE),
+    timed end to end: H2D of the page-locked inputs, the kernels, the gather (PCIe-inclusive; never
+    `value`). Checked against the timed batch's results (Dice#match + #confidence)."""
+    import torch
+    from licensee_amd._native import (DICE_GATHER_DEVICE, DICE_GATHER_HOST, FileBatch, Scorer, last_gather_peer,
+                                      match_sharded)
+    n_ctx = max(1, args.abi_contexts or n_dev)
+    devices = [i % max(n_dev, 1) for i in range(n_ctx)]
+    c, f = run.corpus, run.files
+    scorers = [Scorer(c.lf_bits, c.lf_size, c.fields_set_size, c.length_slack, c.length, c.is_cc, n_vocab=c.n_vocab,
+                      device=d) for d in devices]
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()
+    files = FileBatch(pin(f.bits), pin(f.wordset_size), pin(f.length), pin(f.cc_false_positive))
+    n = files.n
+    outs = (pin(np.empty(n, np.int32)), pin(np.empty(n, np.uint32)), pin(np.empty(n, np.float64)))
+    # expected: the resident batch through dice_batch_match_confidence
+    run.batch.match(args.threshold, confidence=True)
+    torch.cuda.synchronize()
+    eb, eo, es = run.batch.download_match()
+    rec = {'entry_point': 'dice_match_sharded_confidence', 'contexts': n_ctx, 'devices': devices, 'files': n,
+           'input': 'page-locked host arrays (dice_files), results into page-locked host arrays'}
+    try:
+        for name, mode in (('host', DICE_GATHER_HOST), ('device', DICE_GATHER_DEVICE)):
+            match_sharded(scorers, files, args.threshold, gather=mode, confidence=True, out=outs)   # warm
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                match_sharded(scorers, files, args.threshold, gather=mode, confidence=True, out=outs)
+                ts.append(time.perf_counter() - t0)
+            ms = float(np.median(ts)) * 1e3
+            mism = int(np.sum(outs[0] != eb) + np.sum(outs[1] != eo) + np.sum(outs[2] != es))
+            rec[name] = {'ms_per_call': ms, 'files_per_s': n / (ms * 1e-3), 'mismatches': mism,
+                         'dice_last_gather_peer': last_gather_peer()}
+        rec['winner'] = 'host' if rec['host']['ms_per_call'] <= rec['device']['ms_per_call'] else 'device'
+        rec['note'] = ('PCIe-inclusive (inputs start in host memory, as the FFI hands them over); the kernel-only rate '
+                       'is `value`. dice_last_gather_peer: 1 = every remote shard written over xGMI peer access, '
+                       '0 = some staged, -1 = host gather')
+    finally:
+        for sc in scorers:
+            sc.close()
+    return rec
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -477,6 +615,12 @@ def main():
     ap.add_argument('--corpus', default='synthetic', choices=['synthetic', 'spdx'],
                     help="config 3's templates: synthetic, or the 94 real texts (47 choosealicense.com + 47 SPDX "
                          "license-list-XML) + synthetic ones")
+    ap.add_argument('--shard-mode', choices=('auto', 'ranks', 'abi'), default='auto',
+                    help="abi: also time the one-process multi-device entry point (dice_match_sharded_confidence, "
+                         "host vs device gather, extras.abi_sharded) at world size 1; auto: that leg with the "
+                         "extras at world size 1; ranks: never")
+    ap.add_argument('--abi-contexts', type=int, default=0,
+                    help='contexts of the abi leg (default: one per visible device)')
     ap.add_argument('--no-extras', action='store_true',
                     help='skip the separately reported host-side rates (PCIe end-to-end, host prep, single-file '
                          'calls): profiling runs then trace only the timed workload')
@@ -548,31 +692,10 @@ def main():
     if not matrix_mode:
         t_g = time.perf_counter()
         best, ov, score = batch.download_match(sptr)
-        host_gather_s = time.perf_counter() - t_g
-        extras['host_gather_ms'] = host_gather_s * 1e3
+        extras['host_gather_ms'] = (time.perf_counter() - t_g) * 1e3
         extras['matches'] = int(group.reduce([int((best >= 0).sum())], 'sum')[0])
-        if distributed:
-            host_gather_s = group.reduce([host_gather_s], 'max')[0]
-            extras['host_gather_ms'] = host_gather_s * 1e3
-            if group.backend == 'nccl':
-                # RCCL alternative: all_gather the 16-B/file results over xGMI (zero-copy views of
-                # the library's result buffers, packed on the device: licensee_amd/shard.py)
-                from licensee_amd.shard import device_results_packed
-                res = device_results_packed(batch)
-                out = torch.empty((world * n_per, 4), dtype=torch.int32, device='cuda')
-                torch.cuda.synchronize()
-                dist.barrier()
-                t_g = time.perf_counter()
-                dist.all_gather_into_tensor(out, res)
-                torch.cuda.synchronize()
-                rccl_s = group.reduce([time.perf_counter() - t_g], 'max')[0]
-                del out
-                extras['rccl_allgather_ms'] = rccl_s * 1e3
-                extras['gather_winner'] = 'host' if host_gather_s <= rccl_s else 'rccl'
-            else:
-                extras['gather_winner'] = 'host'
-                extras['gather_note'] = 'ranks share a device: no RCCL communicator, host gather only'
-
+        if distributed and world > 1:
+            extras.update(gather_compare(batch, group, rank, world, n_per, best, ov, score, sptr))
     # ---- separately reported rates (never `value`): PCIe-inclusive end-to-end, host prep ----
     if rank == 0 and not matrix_mode and not args.probe and not args.no_extras:
         torch.cuda.synchronize()
@@ -651,6 +774,12 @@ def main():
                                   'exact_matches': int((ex >= 0).sum()),
                                   'note': 'dice_batch_exact over the resident batch (kernel only, no field-mask '
                                           'upload): Exact#match for every file beside the Dice pass'}
+
+    if world == 1 and not matrix_mode and not args.probe and (
+            args.shard_mode == 'abi' or (args.shard_mode == 'auto' and not args.no_extras)):
+        torch.cuda.synchronize()
+        extras['abi_sharded'] = abi_sharded_leg(run, args, n_dev)
+        log(f"abi sharded: {extras['abi_sharded']}")
 
     cpu_baseline = None
     parity = None

@@ -476,16 +476,23 @@ def _ctx_array(scorers):
 
 
 def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DICE_GATHER_HOST,
-                  confidence: bool = False):
+                  confidence: bool = False, out=None):
     """``dice_match_sharded`` (``dice_match_sharded_confidence`` with confidence=True): the files
     split into contiguous shards, one per Scorer (each on its own device, host thread and stream),
     results gathered on the host or on the first Scorer's device. Every Scorer must hold the same
-    corpus."""
+    corpus. ``out``: optional (best int32, overlap uint32, score float64) [n] arrays to fill (e.g.
+    page-locked buffers, which the gathers copy into directly)."""
     arr, n_ctx, _ = _ctx_array(scorers)
     n = files.n
-    best = np.empty(n, np.int32)
-    ov = np.empty(n, np.uint32)
-    score = np.empty(n, np.float64)
+    if out is not None:
+        best, ov, score = out
+        if not (best.dtype == np.int32 and ov.dtype == np.uint32 and score.dtype == np.float64 and
+                best.shape == ov.shape == score.shape == (n,) and all(a.flags.c_contiguous for a in out)):
+            raise ValueError('out must be contiguous [n] int32 / uint32 / float64 arrays')
+    else:
+        best = np.empty(n, np.int32)
+        ov = np.empty(n, np.uint32)
+        score = np.empty(n, np.float64)
     if n:
         st = files._struct()
         lib = load_library()

@@ -71,6 +71,11 @@ struct Partials {
 #ifndef POST_DENSE_LDS_PREFIX
 #define POST_DENSE_LDS_PREFIX 1
 #endif
+// The walk's padding entries go to per-lane sinks instead of exec-masked adds (count_or_sink; 0:
+// the masked form, A/B)
+#ifndef POST_WALK_SINK
+#define POST_WALK_SINK 1
+#endif
 constexpr int kPostWaves = 16;
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
@@ -83,11 +88,34 @@ constexpr int word_cap() { return TPMAX <= 608 ? 416 : 320; }
 constexpr uint16_t kNoTpl = 0xFFFF;      // empty row entry
 constexpr uint16_t kMore = 0xFFFE;       // row entry 15: a long word (entries 0-1 offset, 2 length)
 constexpr int kLongCap = 64;             // per-wave queue of long words (offset, length)
-constexpr int kChunks = 3;               // 64-word chunks of a file loaded together
+// 64-word chunks of a file loaded together (match / matrix kernel)
+#ifndef POST_CHUNKS_MATCH
+#define POST_CHUNKS_MATCH 6
+#endif
+#ifndef POST_CHUNKS_MATRIX
+#define POST_CHUNKS_MATRIX 6
+#endif
 
 // Postings entries are byte offsets (4 * template) into the wave's u32 counter row.
 __device__ __forceinline__ void count(uint32_t* crow32, uint32_t off) {
     atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(crow32) + off), 1u);
+}
+
+// LDS byte addresses as integers (address space 3 is 32-bit), and a counter add at one.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(uint32_t* p) { return (uint32_t)(uintptr_t)(lds_u32*)p; }
+__device__ __forceinline__ void lds_inc(uint32_t a) {
+    __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// A postings row entry added without a branch: the address min(counter row + entry, sink) is the
+// template's counter for a real entry (byte offset < 4 * TPMAX) and the lane's own sink dword for
+// padding (0xFFFF) and the long-word marker (0xFFFE) -- the sink lies past every counter row and
+// less than 0xFFFE bytes above any of them (the narrow kernel's LDS layout, post_narrow_body), so
+// an entry costs one v_add (SDWA half select) + one v_min + the ds_add, instead of a compare and
+// an exec mask round trip per entry. Sinks are per lane (distinct banks: no same-address
+// serialization) and are queue slots whose words were already read (walk_short).
+__device__ __forceinline__ void count_or_sink(uint32_t cbase, uint32_t sink, uint32_t entry) {
+    lds_inc(min(cbase + entry, sink));
 }
 
 // Long words (> 16 narrow postings): 64 lanes per word, 4 words' id loads in flight.
@@ -130,6 +158,7 @@ __device__ __forceinline__ void load_rows(const uint32_t* wq, uint32_t nq, uint3
     }
 }
 
+template <int WCAP>
 __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint2* lq, uint32_t& nl,
                                            const uint16_t* __restrict__ prow,
                                            const uint16_t* __restrict__ plong, uint32_t* crow32, int lane) {
@@ -149,6 +178,21 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
             nl = rfl(nl + (uint32_t)__builtin_popcountll(bl));
             if (lng) r0 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
         }
+#if POST_WALK_SINK
+        // this pass's queue slots [e0, e0 + 64) were read a pass ago: lane l's sink is slot e0 + l,
+        // or slot WCAP - 64 + l in a last pass that starts past WCAP - 64 (those slots were read
+        // too, and no later pass exists: nq <= WCAP)
+        const uint32_t cbase = lds_addr(crow32),
+                       sink = lds_addr(const_cast<uint32_t*>(wq) + min(e0, (uint32_t)(WCAP - kWave))) + 4u * (uint32_t)lane;
+        const uint32_t rr[4] = {r0.x, r0.y, r0.z, r0.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) count_or_sink(cbase, sink, (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+        if (__ballot(mid)) {   // entries 8-15 (0xFFFF padding / the long marker for other words: sinks)
+            const uint32_t r2[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) count_or_sink(cbase, sink, (r2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+        }
+#else
         const uint32_t rr[4] = {r0.x, r0.y, r0.z, r0.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -163,6 +207,7 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
                 if (mid && id < kMore) count(crow32, id);
             }
         }
+#endif
         if (nl > kLongCap - kWave) walk_long(lq, nl, plong, crow32, lane);
         w = wn;
         r0 = n0;
@@ -493,6 +538,7 @@ __device__ __forceinline__ void load_partials(const Partials& pt, int64_t pos, i
     }
 }
 
+template <int kChunks>
 __device__ __forceinline__ void load_chunks(const uint64_t* __restrict__ row, int32_t w64, int32_t pb, int lane,
                                             uint64_t (&xs)[kChunks]) {
 #pragma unroll
@@ -506,7 +552,7 @@ __device__ __forceinline__ void load_chunks(const uint64_t* __restrict__ row, in
 // gives every lane its queue slots, and each lane writes its own words (a chunk of more than
 // WCAP words -- a file holding most of the vocabulary -- goes round by round instead); a full
 // queue is walked.
-template <int WCAP>
+template <int WCAP, int kChunks>
 __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int32_t pb, uint32_t* wq, uint32_t& nq,
                                              uint2* lq, uint32_t& nl, const uint16_t* __restrict__ prow,
                                              const uint16_t* __restrict__ plong, uint32_t* crow32, int lane) {
@@ -519,7 +565,7 @@ __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int3
         const uint32_t total = rfl(__builtin_amdgcn_readlane(incl, kWave - 1));
         if (total == 0) continue;
         if (nq + total > WCAP) {
-            if (!(POST_DIAG & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
+            if (!(POST_DIAG & 2)) walk_short<WCAP>(wq, nq, lq, nl, prow, plong, crow32, lane);
             nq = 0;
         }
         if (total <= WCAP) {
@@ -539,7 +585,7 @@ __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int3
             if (has) wq[nq + lane_rank(bal)] = w;
             nq = rfl(nq + (uint32_t)__builtin_popcountll(bal));
             if (nq > WCAP - kWave) {
-                if (!(POST_DIAG & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
+                if (!(POST_DIAG & 2)) walk_short<WCAP>(wq, nq, lq, nl, prow, plong, crow32, lane);
                 nq = 0;
             }
         }
@@ -551,7 +597,7 @@ __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int3
 // here, before its first word chunks, and copied in once those are requested -- instead of being
 // prefetched into registers during the previous file's scoring, where the matrix kernel cannot
 // afford them.
-template <int WCAP, bool LATE, int PJ>
+template <int WCAP, bool LATE, int PJ, int kChunks = LATE ? POST_CHUNKS_MATRIX : POST_CHUNKS_MATCH>
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
                                               const Partials& pt, int64_t pos, bool wide, int32_t tp, uint32_t* wq,
                                               uint2* lq,
@@ -567,18 +613,18 @@ __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, 
     if (LATE) {
         uint32_t part[PJ];
         load_partials<PJ, true>(pt, pos, tp, wide, lane, part);
-        if (pb < w64) load_chunks(row, w64, pb, lane, xs);
+        if (pb < w64) load_chunks<kChunks>(row, w64, pb, lane, xs);
         copy_in<PJ>(crow32, part, tp, wide, lane);
         if (pb < w64) {
-            queue_chunks<WCAP>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
+            queue_chunks<WCAP, kChunks>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
             pb += kChunks * kWave;
         }
     }
     for (; pb < w64; pb += kChunks * kWave) {
-        load_chunks(row, w64, pb, lane, xs);
-        queue_chunks<WCAP>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
+        load_chunks<kChunks>(row, w64, pb, lane, xs);
+        queue_chunks<WCAP, kChunks>(xs, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
     }
-    if (!(POST_DIAG & 2)) walk_short(wq, nq, lq, nl, prow, plong, crow32, lane);
+    if (!(POST_DIAG & 2)) walk_short<WCAP>(wq, nq, lq, nl, prow, plong, crow32, lane);
     walk_long(lq, nl, plong, crow32, lane);
 }
 
@@ -814,9 +860,15 @@ __device__ __forceinline__ void post_narrow_body(
     constexpr int kTJ = (TPMAX + kWave - 1) / kWave;           // templates per lane
     constexpr int kWCap = word_cap<TPMAX>();
     constexpr int kPJ = pairs_per_lane<TPMAX>();
-    __shared__ uint32_t cnt32[kPostWaves * TPMAX];             // u32 counters, one row per wave
+    // u32 counters, one row per wave, then the queues of narrow word ids: one array, so the queue
+    // slots (the walk's sinks, count_or_sink) lie past every counter row and within 64 KiB of it
+    __shared__ uint32_t cntq[kPostWaves * TPMAX + kPostWaves * kWCap];
+    // (wave w's sinks end 4 (16 TPMAX + (w + 1) WCAP) bytes in, its row starts at 4 w TPMAX: the
+    // largest gap is wave 0's)
+    static_assert(kWCap <= TPMAX && (kPostWaves * TPMAX + kWCap) * 4 <= 0xFFFE, "sinks within reach of every row");
+    uint32_t* const cnt32 = cntq;
+    uint32_t (*const wq)[kWCap] = reinterpret_cast<uint32_t (*)[kWCap]>(cntq + kPostWaves * TPMAX);
     __shared__ uint2 tcs[TPMAX];                               // packed template constants
-    __shared__ uint32_t wq[kPostWaves][kWCap];                 // queued narrow word ids
     __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
     __shared__ uint2 tsc[kMatrix ? kPostWaves : 1][kPostFiles / kPostWaves];   // matrix: own files' {|W_F|, len_F}
     const int lane = threadIdx.x & (kWave - 1);

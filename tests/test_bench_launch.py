@@ -57,10 +57,30 @@ def test_bench_two_ranks_on_one_gpu():
     assert line['extras']['process_group']['world_size'] == 2
     assert line['cpu_baseline'] and line['cpu_baseline']['value'] > 0
     assert line['parity']['mismatches'] == 0 and line['parity']['ranks_checked'] == 2
+    # the host gather: both ranks' results in rank 0's shared host buffer, checked
+    ex = line['extras']
+    assert ex['host_gather_mismatches'] == 0 and ex['host_gather_checked'] is True, ex
+    assert ex['gather_winner'] == 'host' and 'no RCCL' in ex['gather_note'] and ex['host_gather_ms'] > 0
     for tag in ('3', '3-top1', '3-allpairs', '5'):
         rec = line['extras']['configs'][tag]
         assert rec['global_files'] == 40000 and rec['parity']['mismatches'] == 0, (tag, rec)
         assert rec['cpu_baseline']['value'] > 0
+
+
+@pytest.mark.gpu
+def test_bench_abi_sharded_leg_three_contexts():
+    """--shard-mode abi: dice_match_sharded_confidence over 3 contexts (all on device 0 of the test
+    box), host and device gathers timed, results equal to the resident batch's."""
+    cmd = [sys.executable, 'bench.py', '--steps', '3', '--warmup', '1', '--files-per-gpu', '50000',
+           '--extra-configs=', '--no-extras', '--no-cpu-baseline', '--shard-mode', 'abi', '--abi-contexts', '3']
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])['extras']['abi_sharded']
+    assert rec['contexts'] == 3 and rec['devices'] == [0, 0, 0] and rec['files'] == 50000
+    for mode in ('host', 'device'):
+        assert rec[mode]['mismatches'] == 0 and rec[mode]['files_per_s'] > 0, rec
+    assert rec['host']['dice_last_gather_peer'] == -1 and rec['device']['dice_last_gather_peer'] in (0, 1)
+    assert rec['winner'] in ('host', 'device')
 
 
 def test_config3_traffic_file_per_entry_point():
