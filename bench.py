@@ -400,16 +400,28 @@ def measure_extra(r, c, args, stream, sptr, cpu, group):
     w, lm, ach = timed(r, steps, 2, stream, group)
     tr, tr_src = traffic_for(c if c != '5-T600' else '5_T600', r.n_per, r.T, traffic_variant(c, r))
     files = r.n_per * group.world
-    rec = {'workload': WORKLOADS[c], 'files_per_gpu': r.n_per, 'global_files': files, 'templates': r.T,
+    # exact-scored pairs per launch, counted on the device (dice_batch_scored_pairs: the pruned
+    # kernel's exact scores + every pair of its deferred files; n * T for the other kernels)
+    scored = r.n_per * r.T if r.cfg == 5 else r.batch.scored_pairs(sptr)
+    scored = int(group.reduce([scored], 'sum')[0])
+    workload = WORKLOADS[c]
+    if r.cfg == 3 and r.match_kernel == 4:
+        workload += (' -- entry point dice_batch_match_confidence (Dice#match + #confidence; rounds 1-3 measured '
+                     'dice_batch_match: see 3-top1)' if r.confidence else ' -- entry point dice_batch_match (top '
+                     'template of every file; the like-for-like figure of rounds 1-3)')
+    rec = {'workload': workload, 'files_per_gpu': r.n_per, 'global_files': files, 'templates': r.T,
            'vocab': r.V, 'kernel': KERNELS[r.match_kernel], 'steps': steps, 'files_per_s': files * steps / w,
-           'scores_per_s': files * steps / w * r.T, 'launch_ms': lm,
+           'decided_pairs_per_s': files * steps / w * r.T, 'exact_scored_pairs_per_launch': scored,
+           'exact_scored_pairs_per_s': scored * steps / w, 'launch_ms': lm,
            'algorithmic_bytes_per_file': r.algo_bytes_per_file, 'roofline_achieved_gbs': ach,
            'roofline_frac': ach / HBM_PEAK_GBS, 'traffic': tr, 'traffic_source': tr_src}
     if r.match_kernel == 4:
         rec['note'] = ('bound-pruned Dice#match: every (file, template) pair is decided, but only pairs whose '
                        'overlap bound can reach the threshold (dice_batch_match_confidence: Dice#match + '
                        '#confidence, dice.rb:8-14,51-53) or the top score (3-top1: dice_batch_match) are scored '
-                       'exactly (DESIGN.md 4); scores_per_s counts decided pairs. 3-allpairs scores every pair')
+                       'exactly (DESIGN.md 4); decided_pairs_per_s counts every (file, template) pair decided, '
+                       'exact_scored_pairs_per_s only those whose overlap was computed (device count). 3-allpairs '
+                       'scores every pair')
         rec['entry_point'] = 'dice_batch_match_confidence' if r.confidence else 'dice_batch_match'
         rec['deferred_files'] = int(group.reduce([r.batch.deferred(sptr)], 'sum')[0])
     if not args.no_cpu_baseline:
@@ -679,6 +691,10 @@ def main():
     sptr = stream.cuda_stream
     wall, launch_ms, achieved = timed(run, args.steps, args.warmup, stream, group)
     total_files = n_per * world
+    exact_pairs = None
+    if not args.probe:
+        exact_pairs = n_per * run.T if matrix_mode else run.batch.scored_pairs(sptr)
+        exact_pairs = int(group.reduce([exact_pairs], 'sum')[0])
     value = total_files * args.steps / wall
     traffic, traffic_src = traffic_for(cfg if cfg != '5-T600' else '5_T600', n_per, run.T, traffic_variant(cfg, run))
     batch, files, corpus, synth = run.batch, run.files, run.corpus, run.synth
@@ -875,7 +891,8 @@ def main():
                                               '(per-GPU roofline; every rank runs the same shard size)'}
                             if world > 1 else {})},
             'cpu_baseline': cpu_baseline,
-            'scores_per_s': value * head['templates'],
+            'decided_pairs_per_s': value * head['templates'],
+            'exact_scored_pairs_per_s': exact_pairs * args.steps / wall if exact_pairs is not None else None,
             'parity': parity,
             'extras': extras,
         }

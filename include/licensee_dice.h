@@ -184,6 +184,12 @@ int dice_batch_match_confidence(dice_batch *batch, double threshold, void *strea
 /* Introspection after dice_batch_match (synchronizes `stream`): files the bound-pruned kernel
  * deferred to the postings kernels in the last call (0 for other kernels). */
 int dice_batch_deferred(dice_batch *batch, int64_t *deferred, void *stream);
+/* Introspection after dice_batch_match / dice_batch_match_confidence (synchronizes `stream`): the
+ * (file, template) pairs whose overlap the last call computed exactly -- n * T for every kernel
+ * but the bound-pruned one (T > 64 match), which scores only the templates whose bound reaches
+ * the running best (or the threshold, confidence mode) and every pair of the files it deferred.
+ * The pairs the bound rules out are decided without a score (dice.rb:34-48 only reads the top). */
+int dice_batch_scored_pairs(dice_batch *batch, int64_t *pairs, void *stream);
 /* Device-resident matrix results are template-major ([T][n] overlap/score, [k][n] top-k) so
  * every store is coalesced; dice_batch_download_matrix returns them row-major. */
 int dice_batch_matrix(dice_batch *batch, int32_t k, void *stream);

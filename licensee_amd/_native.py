@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     'dice_batch_deferred',
     'dice_ctx_match_kernel', 'dice_exact_setup', 'dice_batch_exact', 'dice_batch_download_exact', 'dice_exact',
     'dice_match_confidence', 'dice_batch_match_confidence', 'dice_match_sharded_confidence',
+    'dice_batch_scored_pairs',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -187,6 +188,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                                           vp, vp]),
         'dice_last_gather_peer': (i32, []),
         'dice_batch_deferred': (ctypes.c_int, [vp, ctypes.POINTER(i64), vp]),
+        'dice_batch_scored_pairs': (ctypes.c_int, [vp, ctypes.POINTER(i64), vp]),
         'dice_precompile': (ctypes.c_int, [ctypes.POINTER(_Templates), ctypes.c_char_p, i32]),
         'dice_program_source': (i64, [ctypes.POINTER(_Templates), ctypes.c_char_p, i64]),
         'dice_exact_setup': (ctypes.c_int, [vp, vp, vp, vp]),
@@ -453,6 +455,13 @@ class DeviceBatch:
         """Files the bound-pruned kernel handed to the postings kernels in the last match."""
         v = ctypes.c_int64(0)
         _check(load_library().dice_batch_deferred(self._b, ctypes.byref(v), ctypes.c_void_p(stream) if stream else None))
+        return int(v.value)
+
+    def scored_pairs(self, stream: int = 0) -> int:
+        """(file, template) pairs the last match call scored exactly (dice_batch_scored_pairs)."""
+        v = ctypes.c_int64(0)
+        _check(load_library().dice_batch_scored_pairs(self._b, ctypes.byref(v),
+                                                      ctypes.c_void_p(stream) if stream else None))
         return int(v.value)
 
     def result_ptrs(self):

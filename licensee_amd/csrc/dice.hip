@@ -489,7 +489,7 @@ void dice_batch_destroy(dice_batch* b) {
     }
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
                     b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
-                    b->d_defer, b->d_ndefer, b->d_exact, b->d_fmask};
+                    b->d_defer, b->d_ndefer, b->d_nscored, b->d_qctr, b->d_exact, b->d_fmask};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -655,12 +655,14 @@ static int batch_match(dice_batch* b, double thr, void* stream, bool confidence)
         int rc = c->prune ? dice::prune_launch_match(c, b, thr, s, confidence)
                           : dice::post_launch_match(c, b, thr, s, confidence);
         if (rc != DICE_OK) return rc;
+        b->last_match = c->prune ? 2 : 1;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
                            c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
                            b->d_ov, b->d_score);
     }
     HIP_TRY(hipGetLastError());
+    if (c->kind != 3) b->last_match = 1;
     if (confidence && c->kind != 3) {
         hipLaunchKernelGGL(dice_confidence_outputs, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0, s, b->d_best,
                            b->d_ov, b->d_score, b->n);
@@ -815,6 +817,28 @@ int dice_batch_deferred(dice_batch* b, int64_t* deferred, void* stream) {
     HIP_TRY(hipMemcpyAsync(&m, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *deferred = m;
+    return DICE_OK;
+}
+
+int dice_batch_scored_pairs(dice_batch* b, int64_t* pairs, void* stream) {
+    if (!b || !pairs) return fail(DICE_E_ARG, "NULL batch/output");
+    *pairs = 0;
+    dice_ctx* c = b->ctx;
+    if (b->last_match == 1) {
+        *pairs = b->n * (int64_t)c->T;   // every kernel but the bound-pruned one scores every pair
+    } else if (b->last_match == 2) {
+        // the pruned kernel's exact scores (per-wave counts) + every pair of each deferred file
+        // (the postings kernels score them all)
+        DeviceGuard g(c->device);
+        hipStream_t s = pick_stream(c, stream);
+        std::vector<uint32_t> h((size_t)b->prune_waves + 1);
+        HIP_TRY(hipMemcpyAsync(h.data(), b->d_nscored, (size_t)b->prune_waves * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h.data() + b->prune_waves, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        int64_t sum = 0;
+        for (int64_t i = 0; i < b->prune_waves; ++i) sum += h[(size_t)i];
+        *pairs = sum + (int64_t)h[(size_t)b->prune_waves] * c->T;
+    }
     return DICE_OK;
 }
 

@@ -82,8 +82,8 @@ struct dice_ctx {
     void* d_ptc = nullptr;     // [T] int4 template constants
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_ld = 0;
     bool post_fast = false;
-    bool post_mfma = true;
-    int32_t post_mfma_mt = 3;  // 32-file M-tiles per MFMA tile (T <= 640; DICE_POST_MFMA_MT=2 for A/B)     // dense prefix by dice_post_dense_mfma (DICE_POST_MFMA=0: the VALU kernel)
+    int32_t post_mfma = 4;     // dense prefix: 4 dice_post_dense_mfma FP4 (default), 1 its int8 form, 0 the VALU kernel (DICE_POST_MFMA)
+    int32_t post_mfma_mt = 3;  // 32-file M-tiles per MFMA tile (T <= 640; DICE_POST_MFMA_MT=2 for A/B)
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --
     // group bytes, constants, CC masks, template index | record offset, records, slot bounds
@@ -172,6 +172,10 @@ struct dice_batch {
     // pruned match (dice_prune.hip): files deferred to the postings kernels
     int32_t* d_defer = nullptr;     // [capacity] file indices
     uint32_t* d_ndefer = nullptr;   // count
+    uint32_t* d_qctr = nullptr;     // sparse-program tile-queue counters (DICE_PROG_QUEUE A/B)
+    uint32_t* d_nscored = nullptr;  // per wave of the last pruned launch: (file, template) pairs scored exactly
+    int64_t prune_waves = 0;        // waves of that launch (entries of d_nscored)
+    int32_t last_match = 0;         // last match call: 0 none, 1 every pair scored, 2 bound-pruned
     // Exact matcher (dice_batch_exact, lazily allocated): per-file result, field masks
     int32_t* d_exact = nullptr;
     uint64_t* d_fmask = nullptr;

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <vector>
 
@@ -375,11 +376,33 @@ __device__ __forceinline__ v4i widen_half(uint32_t v, int h) {
     return r;
 }
 
+// FP4 variant (DICE_POST_MFMA=4): the block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1
+// operands takes a whole u64 prefix word per instruction (K = 64: lane half h holds the word's
+// bits [32 h, 32 h + 32) as 32 nibbles). Bit -> nibble: dword k of the fragment = (v >> k) &
+// 0x11111111, i.e. nibble i = bit 4 i + k (one VALU per dword after the first shift; A and B
+// share the permutation, so every product pairs one bit of the file with the same bit of the
+// template). Nibble 0b0001 is e2m1 0.5 and both block scales are 2^1 (E8M0 0x80), so each
+// product is exactly 1.0 and the f32 accumulator holds the integer count (<= 1024, exact). Half
+// the widening VALU and half the MFMAs of the int8 form per prefix bit (the FP4 rate is twice
+// the int8 rate per clock on gfx950: 32 cycles for 32 x 32 x 64).
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ v8i widen_nibbles(uint32_t v) {
+    v8i r;
+    r[0] = (int)(v & 0x11111111u);
+    r[1] = (int)((v >> 1) & 0x11111111u);
+    r[2] = (int)((v >> 2) & 0x11111111u);
+    r[3] = (int)((v >> 3) & 0x11111111u);
+    r[4] = r[5] = r[6] = r[7] = 0;   // (fp4 operands use the first four registers)
+    return r;
+}
+constexpr int kE8M0Two = 0x80808080;   // block scale 2^1 in every byte
+
 // A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one M-tile at
 // a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as whole
 // 128-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94).
-template <int NTW, int MT>
-__device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[MT][NTW], uint16_t* slab, uint16_t* __restrict__ part,
+template <int NTW, int MT, class ACC>
+__device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][NTW], uint16_t* slab, uint16_t* __restrict__ part,
                                                 int64_t f0, int64_t nn, int32_t tb, int32_t te, int32_t tp, int lane) {
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
@@ -390,7 +413,7 @@ __device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[MT][NTW], uint
         for (int j = 0; j < NTW; ++j)
 #pragma unroll
             for (int g = 0; g < 16; ++g)
-                slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + 32 * j + rf] = (uint16_t)acc[m][j][g];
+                slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + 32 * j + rf] = (uint16_t)(uint32_t)acc[m][j][g];
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -404,7 +427,7 @@ __device__ __forceinline__ void mfma_store_tile(const v16i (&acc)[MT][NTW], uint
     }
 }
 
-template <int DP, int NTW, int NW, int MT>
+template <int DP, int NTW, int NW, int MT, bool F4 = false>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
     const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
@@ -459,11 +482,12 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     for (int buf = 0; f0 < nn; f0 += stride, buf = (buf + 1) % kBufs) {
         const bool more = f0 + stride < nn;   // uniform
         if (more) load_pre(f0 + stride, pv);
-        v16i acc[MT][NTW];
+        using Acc = typename std::conditional<F4, v16f, v16i>::type;
+        Acc acc[MT][NTW];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) acc[m][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            for (int j = 0; j < NTW; ++j) acc[m][j] = Acc{};
         const uint64_t* pb = pre[buf];
         const uint64_t* bcol = bm + tb + r;
 #pragma unroll 2
@@ -474,6 +498,22 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             uint64_t a[MT];
 #pragma unroll
             for (int m = 0; m < MT; ++m) a[m] = pb[(32 * m + r) * kPreStride + q];
+            if constexpr (F4) {
+                // one instruction per (M-tile, N-tile) and word: lane half h holds bits [32 h, 32 h + 32)
+                v8i fa[MT];
+#pragma unroll
+                for (int m = 0; m < MT; ++m) fa[m] = widen_nibbles((uint32_t)(a[m] >> (32 * h)));
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) {
+                    if (j < nw_tiles) {   // uniform
+                        const v8i fb = widen_nibbles((uint32_t)(bw[j] >> (32 * h)));
+#pragma unroll
+                        for (int m = 0; m < MT; ++m)
+                            acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[m], fb, acc[m][j], 4, 4, 0,
+                                                                                         kE8M0Two, 0, kE8M0Two);
+                    }
+                }
+            } else {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 v4i fa[MT];
@@ -488,6 +528,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
                             acc[m][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m], fb, acc[m][j], 0, 0, 0);
                     }
                 }
+            }
             }
         }
         if (kBufs == 1) __syncthreads();   // every wave is done with the one prefix buffer
@@ -1091,8 +1132,11 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     c->post_dense = D;
     c->post_tpad = tpad;
     // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
+    // the dense prefix on the matrix cores, FP4 form (4, default: config 3 all pairs 3.76 -> 3.59 ms,
+    // 5-T600 5.33 -> 5.15 ms against the int8 form, 2 interleaved reps); 1: the int8 form; 0: the
+    // VALU kernel (A/B)
     const char* mf = getenv("DICE_POST_MFMA");
-    c->post_mfma = !(mf && *mf == '0');
+    c->post_mfma = (mf && *mf == '0') ? 0 : (mf && *mf == '1') ? 1 : 4;
     const char* mt = getenv("DICE_POST_MFMA_MT");   // 32-file M-tiles per MFMA tile (2 or 3; A/B)
     c->post_mfma_mt = (mt && *mt == '2') ? 2 : 3;
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
@@ -1135,9 +1179,13 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
         // persistent workgroups (one per CU: 10-11 waves at 3 per SIMD), the next tile's prefixes
         // loaded during this one
         const bool small = c->post_tp <= 640;
-        auto kern = small ? (c->post_mfma_mt == 3 ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3>
-                                                  : dice_post_dense_mfma<DP, kMfmaNT, 12, 2>)
-                          : dice_post_dense_mfma<DP, kMfmaNT, 11, 2>;
+        auto kern = c->post_mfma == 4
+                        ? (small ? (c->post_mfma_mt == 3 ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3, true>
+                                                         : dice_post_dense_mfma<DP, kMfmaNT, 12, 2, true>)
+                                 : dice_post_dense_mfma<DP, kMfmaNT, 11, 2, true>)
+                        : (small ? (c->post_mfma_mt == 3 ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3>
+                                                         : dice_post_dense_mfma<DP, kMfmaNT, 12, 2>)
+                                 : dice_post_dense_mfma<DP, kMfmaNT, 11, 2>);
         const int64_t mtiles = (b->n + 32 * c->post_mfma_mt - 1) / (32 * c->post_mfma_mt);
         const int64_t g = std::min<int64_t>(std::min<int64_t>(groups, mtiles), (int64_t)c->n_cu);
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 12 : 11) * kWave), 0, s,

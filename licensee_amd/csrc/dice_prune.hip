@@ -242,7 +242,7 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
                                             uint32_t sbk, const uint32_t (&fb)[4], uint32_t negwv, uint32_t m2big,
                                             uint32_t lf, uint32_t wf, uint32_t wf4, bool fast, int lane,
                                             uint32_t (&key)[TJ], uint32_t& lane_max, float& llo, int32_t& bi,
-                                            uint32_t& bo, int32_t& bd, PhaseClock& pclk) {
+                                            uint32_t& bo, int32_t& bd, uint32_t& nsc, PhaseClock& pclk) {
     const int32_t t0 = lane + jstar * kWave;
     uint32_t ks = slot_key<BIG, CC, CLAMP>(q8, stc, ccm, t0, (uint32_t)(jstar + 1), T, (jstar + 1) * kWave > T, fb,
                                            negwv, m2big, lf, wf4);
@@ -260,6 +260,7 @@ __device__ __forceinline__ void prune4_keys(const uint4* q8, const uint4* stc, c
             int32_t to;
             const RecHead h = records_head(t1, srec, pa.qrec, lane, to);
             score_template(t1, to, h, pa.qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
+            ++nsc;
         }
         if (lane == l1) ks = 0;
     }
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
     const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
     int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out, bool corpus_fast,
     bool zero_base, uint32_t wf_noclamp, int32_t* __restrict__ defer, uint32_t* __restrict__ ndefer,
-    int32_t max_evals, int32_t route_cands, float llo0, bool conf, uint64_t* __restrict__ diag_out) {
+    int32_t max_evals, int32_t route_cands, float llo0, bool conf, uint32_t* __restrict__ nscored,
+    uint64_t* __restrict__ diag_out) {
     constexpr int kTP = TJ * kWave;
     // route_cands packs the routing point: candidates | exact scores before the test << 16 (0: 2)
     const int32_t route_at = (route_cands >> 16) ? (route_cands >> 16) : 2;
@@ -343,6 +345,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 
     int32_t ri = -2, rd = 1;   // lane l: result of file (block start + l); -2 = none, -3 = deferred
     uint32_t ro = 0;
+    uint32_t nsc = 0;          // (file, template) pairs this wave scored exactly (wave-uniform)
     if (PRUNE_DIAG & 8) pclk.mark(7);
     for (int64_t file = wbeg; file < wend; ++file) {   // wave-uniform
         const int slot = (int)((file - wbeg) & (kWave - 1));
@@ -415,19 +418,19 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                 PHASE(1);
                 if (!big && !ccf && wf >= wf_noclamp)
                     prune4_keys<TJ, false, false, false>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                         lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
+                                                         lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, nsc, pclk);
                 else if (!big && !ccf)
                     prune4_keys<TJ, false, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                        lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
+                                                        lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, nsc, pclk);
                 else if (!big)
                     prune4_keys<TJ, false, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
+                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, nsc, pclk);
                 else if (!ccf)
                     prune4_keys<TJ, true, false, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
+                                                       lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, nsc, pclk);
                 else
                     prune4_keys<TJ, true, true, true>(q8, stc, ccm, srec, pa, myrow, T, jstar, sbk, fb, negwv, m2big,
-                                                      lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, pclk);
+                                                      lf, wf, wf4, fast, lane, key, lmax, llo, bi, bo, bd, nsc, pclk);
                 // the largest remaining key, scored while it can reach the best score (most files:
                 // no key is left at or above the best score, one compare per lane)
                 if (__ballot(lmax != 0 && !(__uint_as_float(lmax) < llo)) != 0)
@@ -459,6 +462,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                     int32_t to;
                     const RecHead h = records_head(ts, srec, pa.qrec, lane, to);
                     score_template(ts, to, h, pa.qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
+                    ++nsc;
                 }
                 PHASE(5);
             }
@@ -503,6 +507,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
                   (uint32_t)__builtin_popcount(nw[j].z) + (uint32_t)__builtin_popcount(nw[j].w);
         PHASE(6);
     }
+    // the wave's exact-score count, one slot per wave (dice_batch_scored_pairs sums them: no atomics)
+    if (lane == 0) nscored[(int64_t)blockIdx.x * NW + wave] = nsc;
     if ((PRUNE_DIAG & 8) && diag_out && lane == 0) {
         const int64_t gw = (int64_t)blockIdx.x * NW + wave;
         for (int k = 0; k < kTPhases; ++k) diag_out[gw * (kTPhases + 1) + k] = pclk.acc[k];
@@ -680,7 +686,8 @@ static int launch_prune(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, f
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows, b->n,
                        per_wave, c->w64, c->T, pa, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score,
                        c->post_fast, c->prune_zero_base, c->prune_wf_noclamp, b->d_defer, b->d_ndefer, max_evals,
-                       route, llo0, conf, diag);
+                       route, llo0, conf, b->d_nscored, diag);
+    b->prune_waves = groups * NW;
     if ((PRUNE_DIAG & 8) && diag) {
         // diagnostic build only: per-phase shader-clock totals over all waves, per file
         std::vector<uint64_t> h((size_t)groups * NW * (kTPhases + 1));
@@ -714,6 +721,9 @@ int prune_reserve(dice_ctx* c, dice_batch* b) {
     int rc;
     if (!b->d_defer && ((rc = dalloc_bytes((void**)&b->d_defer, (size_t)b->capacity * 4)) ||
                         (rc = dalloc_bytes((void**)&b->d_ndefer, 4))))
+        return rc;
+    // one exact-score count per wave of the persistent grid (at most 32 waves per CU)
+    if (!b->d_nscored && (rc = dalloc_bytes((void**)&b->d_nscored, (size_t)std::max(c->n_cu, 1) * 32 * 4 + 64 * 4)))
         return rc;
     return post_reserve(c, b);
 }

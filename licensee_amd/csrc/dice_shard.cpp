@@ -201,10 +201,6 @@ int gather_d2h(dice_ctx* c0, const std::vector<std::pair<void*, size_t>>& outs, 
 
 }  // namespace
 
-extern "C" {
-
-}  // extern "C"
-
 static int match_sharded(dice_ctx* const* ctxs, int32_t n_ctx, const dice_files* f, double thr, int32_t gather,
                          int32_t* best, uint32_t* ov, double* score, bool confidence) {
     int rc = check_ctxs(ctxs, n_ctx, f, gather);

@@ -236,3 +236,33 @@ def test_threshold_equality_sharded_confidence_three_contexts(config3):
     finally:
         for s in scs:
             s.close()
+
+
+def test_scored_pairs_counted_on_device(config3, monkeypatch):
+    """dice_batch_scored_pairs (VERDICT r4 item 5): the postings kernels score every pair (n * T);
+    the bound-pruned kernel scores between its deferred files' pairs and n * T, fewer through the
+    confidence entry point (its drop level starts at the threshold), and the count is the same for
+    two launches of the same batch."""
+    c, fb = config3
+    n, T = fb.n, len(c.templates)
+    for prune in ('0', '1'):
+        monkeypatch.setenv('DICE_POST_PRUNE', prune)
+        sc = _scorer(c)
+        b = sc.batch(n)
+        try:
+            b.upload(fb)
+            b.match(98.0)
+            top1 = b.scored_pairs()
+            b.match(98.0)
+            assert b.scored_pairs() == top1
+            if prune == '0':
+                assert top1 == n * T
+                continue
+            d = b.deferred()
+            assert d * T <= top1 < n * T // 10, (top1, d)
+            b.match(98.0, confidence=True)
+            conf = b.scored_pairs()
+            assert b.deferred() * T <= conf <= top1, (conf, top1)
+        finally:
+            b.close()
+            sc.close()

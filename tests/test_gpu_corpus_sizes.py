@@ -48,10 +48,11 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
     _check_corpus(n_templates, kernel, monkeypatch)
 
 
-# the postings kernels' dense-prefix variants: the matrix-core kernel with 3 or 2
-# 32-file M-tiles per tile (12 waves, tp <= 640) and its 11-wave form above 640 templates (672,
-# 700), and the VALU kernel (DICE_POST_MFMA=0)
-PREFIX_VARIANTS = {'mfma-mt3': {}, 'mfma-mt2': {'DICE_POST_MFMA_MT': '2'}, 'valu': {'DICE_POST_MFMA': '0'}}
+# the postings kernels' dense-prefix variants: the matrix-core kernel (default, int8
+# and FP4 forms) with 3 or 2 32-file M-tiles per tile (12 waves, tp <= 640) and its 11-wave form
+# above 640 templates (672, 700), and the VALU kernel (DICE_POST_MFMA=0)
+PREFIX_VARIANTS = {'fp4-mt3': {}, 'fp4-mt2': {'DICE_POST_MFMA_MT': '2'}, 'valu': {'DICE_POST_MFMA': '0'},
+                   'int8-mt3': {'DICE_POST_MFMA': '1'}, 'int8-mt2': {'DICE_POST_MFMA': '1', 'DICE_POST_MFMA_MT': '2'}}
 
 
 @pytest.mark.parametrize('variant', sorted(PREFIX_VARIANTS))
