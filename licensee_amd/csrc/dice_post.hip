@@ -357,8 +357,9 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // it. (5-T600 dense kernel, step by step: 1.70 ms -> 0.68 ms, the VALU kernel 1.45;
 // profiles/r4_mfma_dense.txt.)
 constexpr int kMfmaNT = 2;       // N-tiles per wave (at most)
-constexpr int kSlabStride = 72;  // u16 per slab row: rows 4 apart (the lane halves) 16 banks apart
+constexpr int kSlabStride = 40;  // u16 per slab row (one 32-template N-tile + 8): rows 4 apart 16 banks apart
 constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>= 11 waves x 2 N-tiles x 32)
+constexpr int kMfmaMaxDense = 20;   // prefix u64 words of the matrix-core kernels (the masks' LDS budget)
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
@@ -398,9 +399,10 @@ __device__ __forceinline__ v8i widen_nibbles(uint32_t v) {
 }
 constexpr int kE8M0Two = 0x80808080;   // block scale 2^1 in every byte
 
-// A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one M-tile at
-// a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as whole
-// 128-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94).
+// A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one (M-tile,
+// N-tile) at a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as
+// 64-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94; a
+// 64-template slab per M-tile needed twice the LDS, which the 20-word masks now use).
 template <int NTW, int MT, class ACC>
 __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][NTW], uint16_t* slab, uint16_t* __restrict__ part,
                                                 int64_t f0, int64_t nn, int32_t tb, int32_t te, int32_t tp, int lane) {
@@ -410,20 +412,22 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][NTW], uint1
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
 #pragma unroll
-        for (int j = 0; j < NTW; ++j)
+        for (int j = 0; j < NTW; ++j) {
+            if (tb + 32 * j >= te) break;   // uniform: the wave's second N-tile may not exist
 #pragma unroll
             for (int g = 0; g < 16; ++g)
-                slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + 32 * j + rf] = (uint16_t)(uint32_t)acc[m][j][g];
-        __builtin_amdgcn_wave_barrier();
+                slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + rf] = (uint16_t)(uint32_t)acc[m][j][g];
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = (lf >> 3) + 8 * i, piece = lf & 7;
-            const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
-            const int64_t file = f0 + 32 * m + row;
-            const int32_t t = tb + piece * 8;
-            if (t < tpf && t < te && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+            for (int i = 0; i < 2; ++i) {
+                const int row = (lf >> 2) + 16 * i, piece = lf & 3;
+                const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
+                const int64_t file = f0 + 32 * m + row;
+                const int32_t t = tb + 32 * j + piece * 8;
+                if (t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+            }
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -434,15 +438,18 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     const uint32_t* __restrict__ pn) {
     // MT 32-file M-tiles per tile; the prefix buffer is doubled when LDS allows (MT = 2), else one
     // buffer and a second barrier per tile
+    static_assert(DP <= kMfmaMaxDense, "prefix wider than the masks' table");
     constexpr int kTF = 32 * MT;                     // files per tile
     constexpr int kBufs = MT == 2 ? 2 : 1;
-    constexpr int kPreStride = kPostMaxDense + 2;   // 18 u64 per file row
-    constexpr int kPreWords = kTF * kPostMaxDense;
+    // DP + 1 u64 per file row (odd: the 32 lanes of a ds_read_b64 column read hit 64 distinct banks)
+    constexpr int kPreStride = DP + 1;
+    constexpr int kPreWords = kTF * DP;
     constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);   // prefix words per thread
     constexpr int kCols = NTW == 2 && NW == 12 ? 640 : NW * NTW * 32;   // the workgroup's template columns
     __shared__ uint64_t pre[kBufs][kTF * kPreStride];
-    __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 88 KiB)
-    __shared__ uint16_t tslab[NW][32 * kSlabStride];  // per-wave transpose of one M-tile (4.5 KiB)
+    __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 110 KiB at DP 20)
+    __shared__ uint16_t tslab[NW][32 * kSlabStride];  // per-wave transpose of one 32 x 32 tile (2.5 KiB)
+    static_assert(sizeof(pre) + sizeof(bm) + sizeof(tslab) <= 160 * 1024, "one workgroup's LDS");
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
@@ -460,7 +467,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const int i = (int)threadIdx.x + k * NW * kWave;
-            const int fi = i / kPostMaxDense, d = i % kPostMaxDense;
+            const int fi = i / DP, d = i % DP;
             const int64_t file = fs + fi;
             pv[k] = (i < kPreWords && file < nn && d < D) ? rows[(idx ? (int64_t)idx[file] : file) * w64 + d] : 0;
         }
@@ -469,7 +476,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const int i = (int)threadIdx.x + k * NW * kWave;
-            if (i < kPreWords) pre[buf][(i / kPostMaxDense) * kPreStride + i % kPostMaxDense] = pv[k];
+            if (i < kPreWords) pre[buf][(i / DP) * kPreStride + i % DP] = pv[k];
         }
     };
     // the masks once per (persistent) workgroup: LDS reads in the k-loop wait on lgkmcnt, so the
@@ -1025,20 +1032,23 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // ---- host side ---------------------------------------------------------------------------
 
 // Estimated per-file cost (wave instructions) of a dense prefix of D u64 words: the dense
-// phase pays T*D*4/64 VALU; every narrow membership a file hits costs ~1/16 of a 6-instruction
-// row walk. A file resembling template t holds t's words, so the expected narrow memberships
-// per file are sum over narrow words of p_w^2 / T (p_w = postings length).
-static int pick_dense(const std::vector<int64_t>& sq_per_u64, int32_t T, int32_t w64) {
+// phase pays T*D*wd per file (VALU kernel: 4/64 -- a v_bcnt pair per template, word and 64-file
+// wave; the FP4 matrix-core kernel: 1/128, eight times less per word, which moves the optimum to
+// the 20-word cap on the config-3 corpus, as measured: DESIGN.md 4); every narrow membership a
+// file hits costs ~1/16 of a 6-instruction row walk. A file resembling template t holds t's
+// words, so the expected narrow memberships per file are sum over narrow words of p_w^2 / T
+// (p_w = postings length).
+static int pick_dense(const std::vector<int64_t>& sq_per_u64, int32_t T, int32_t w64, int maxd, double wd) {
     const char* e = getenv("DICE_POST_DENSE");
-    if (e && *e) return std::max(0, std::min(std::min(kPostMaxDense, w64), atoi(e)));
+    if (e && *e) return std::max(0, std::min(std::min(maxd, w64), atoi(e)));
     double rest = 0;
     for (int64_t v : sq_per_u64) rest += (double)v;
     int best_d = 0;
     double best_c = 0.4 * rest / T;
     double c_dense = 0;
-    for (int d = 1; d <= std::min(kPostMaxDense, w64); ++d) {
+    for (int d = 1; d <= std::min(maxd, w64); ++d) {
         rest -= (double)sq_per_u64[d - 1];
-        c_dense = (double)T * d * 4.0 / 64.0;
+        c_dense = (double)T * d * wd;
         const double c = c_dense + 0.4 * rest / T;
         if (c < best_c) { best_c = c; best_d = d; }
     }
@@ -1070,8 +1080,16 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     }
     std::vector<int64_t> sq((size_t)w64, 0);
     for (int64_t w = 0; w < nbits; ++w) sq[(size_t)(w / 64)] += (int64_t)plen[(size_t)w] * plen[(size_t)w];
-    // the dense phase runs D rounded up to a multiple of 4 anyway (kernel template): use them all
-    const int D = std::min(w64, (pick_dense(sq, T, w64) + 3) / 4 * 4);
+    // the dense prefix on the matrix cores, FP4 form (4, default: config 3 all pairs 3.76 -> 3.59 ms,
+    // 5-T600 5.33 -> 5.15 ms against the int8 form, 2 interleaved reps); 1: the int8 form; 0: the
+    // VALU kernel (A/B)
+    const char* mf = getenv("DICE_POST_MFMA");
+    c->post_mfma = (mf && *mf == '0') ? 0 : (mf && *mf == '1') ? 1 : 4;
+    // the dense phase runs D rounded up to a multiple of 4 anyway (kernel template): use them all;
+    // up to 20 words on the matrix cores, 16 on the VALU kernel (their LDS budgets)
+    const int maxd = c->post_mfma ? kMfmaMaxDense : kPostMaxDense;
+    const double wd = c->post_mfma == 4 ? 1.0 / 128 : c->post_mfma ? 1.0 / 64 : 4.0 / 64;
+    const int D = std::min(std::min(w64, maxd), (pick_dense(sq, T, w64, maxd, wd) + 3) / 4 * 4);
     // one 32-byte postings row per narrow word (u64 words >= D), indexed by word id: a SHORT word
     // (<= 16 templates) lists its template ids ascending, 0xFFFF padding; a LONG word stores its
     // offset into the flat `plong` id list in entries 0-1, its length in entry 2, 0xFFFE in 15
@@ -1104,7 +1122,7 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     // dense prefix masks, template-major [T][kPostMaxDense]; template constants
     std::vector<uint64_t> dm((size_t)T * kPostMaxDense, 0);
     for (int32_t i = 0; i < T; ++i)
-        for (int d = 0; d < D; ++d) dm[(size_t)i * kPostMaxDense + d] = t->lf_bits[(size_t)i * w64 + d];
+        for (int d = 0; d < std::min(D, kPostMaxDense); ++d) dm[(size_t)i * kPostMaxDense + d] = t->lf_bits[(size_t)i * w64 + d];
     // template constants packed for LDS: {length | cc << 31, base | slack << 16} (post_feasible
     // checks the ranges)
     std::vector<uint2> tcv((size_t)T);
@@ -1117,10 +1135,11 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     if ((rc = dalloc_bytes(&c->d_prow, prow.size() * 2)) || (rc = dalloc_bytes(&c->d_povf, plong.size() * 2)) ||
         (rc = dalloc_bytes(&c->d_pdm, dm.size() * 8)) || (rc = dalloc_bytes(&c->d_ptc, tcv.size() * sizeof(uint2))))
         return rc;
-    // the same masks word-major for the MFMA kernel: [q][kMfmaCols], zero for t >= T
-    std::vector<uint64_t> dmt((size_t)kPostMaxDense * kMfmaCols, 0);
+    // the masks word-major for the MFMA kernels: [q][kMfmaCols], q < kMfmaMaxDense, zero for t >= T
+    // and for q >= D
+    std::vector<uint64_t> dmt((size_t)kMfmaMaxDense * kMfmaCols, 0);
     for (int32_t i = 0; i < T; ++i)
-        for (int d = 0; d < kPostMaxDense; ++d) dmt[(size_t)d * kMfmaCols + i] = dm[(size_t)i * kPostMaxDense + d];
+        for (int d = 0; d < D; ++d) dmt[(size_t)d * kMfmaCols + i] = t->lf_bits[(size_t)i * w64 + d];
     if ((rc = dalloc_bytes(&c->d_pdmt, dmt.size() * 8))) return rc;
     if (hipMemcpy(c->d_pdmt, dmt.data(), dmt.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
         return fail(DICE_E_DEVICE, "postings plan upload failed");
@@ -1132,11 +1151,6 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     c->post_dense = D;
     c->post_tpad = tpad;
     // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
-    // the dense prefix on the matrix cores, FP4 form (4, default: config 3 all pairs 3.76 -> 3.59 ms,
-    // 5-T600 5.33 -> 5.15 ms against the int8 form, 2 interleaved reps); 1: the int8 form; 0: the
-    // VALU kernel (A/B)
-    const char* mf = getenv("DICE_POST_MFMA");
-    c->post_mfma = (mf && *mf == '0') ? 0 : (mf && *mf == '1') ? 1 : 4;
     const char* mt = getenv("DICE_POST_MFMA_MT");   // 32-file M-tiles per MFMA tile (2 or 3; A/B)
     c->post_mfma_mt = (mt && *mt == '2') ? 2 : 3;
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
@@ -1193,10 +1207,12 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
                            (const uint64_t*)c->d_pdmt, partials_of(c, b).p16, idx, pn);
         return;
     }
-    auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
-                       (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
-                       (const uint64_t*)c->d_pdm, partials_of(c, b), idx, pn);
+    if constexpr (DP <= kPostMaxDense) {   // (the VALU kernel's prefix is capped at 16 words: post_setup)
+        auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
+                           (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
+                           (const uint64_t*)c->d_pdm, partials_of(c, b), idx, pn);
+    }
 }
 
 int post_reserve(dice_ctx* c, dice_batch* b) {
@@ -1238,7 +1254,8 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
             case 1: launch_dense<4>(c, b, s, groups, idx, pn); break;
             case 2: launch_dense<8>(c, b, s, groups, idx, pn); break;
             case 3: launch_dense<12>(c, b, s, groups, idx, pn); break;
-            default: launch_dense<16>(c, b, s, groups, idx, pn); break;
+            case 4: launch_dense<16>(c, b, s, groups, idx, pn); break;
+            default: launch_dense<20>(c, b, s, groups, idx, pn); break;
         }
     }
     auto kern = c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608> : dice_post_narrow_match<608>)

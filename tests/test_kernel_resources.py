@@ -4,7 +4,8 @@ The postings kernels and the config-3 pruned kernel are written for 8 waves per 
 two 16-wave workgroups per CU). A kernel that spills to scratch pays a reload whose vmcnt(0) waits
 for every store and load issued before it ("Matrix kernel without spills"): keep
 them at zero scratch and full occupancy. The matrix-core dense-prefix kernel holds 64 i32
-accumulators per lane and runs at 3 waves per SIMD, also without scratch."""
+accumulators per lane (int8 form; f32 in the FP4 form) and runs at 3 waves per SIMD, also without
+scratch."""
 import os
 import sys
 
@@ -44,7 +45,10 @@ def test_config3_pruned_kernel_fits_8_waves_without_scratch():
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
 def test_mfma_dense_prefix_kernel_fits_2_waves_without_scratch():
     res = _resources('dice_post.hip')
-    for name in ('dice_post_dense_mfma<16, 2, 12, 2>', 'dice_post_dense_mfma<16, 2, 12, 3>', 'dice_post_dense_mfma<16, 2, 11, 2>'):
+    # int8 (false) and FP4 (true) forms; the FP4 kernel at the 20-word prefix the config-3 corpus uses
+    names = [f'dice_post_dense_mfma<{dp}, 2, {nw}, {mt}, {f4}>' for dp, f4 in ((16, 'false'), (16, 'true'), (20, 'true'))
+             for nw, mt in ((12, 2), (12, 3), (11, 2))]
+    for name in names:
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0' and r['VGPRs Spill'] == '0', (name, r)
         assert int(r['Occupancy [waves/SIMD]']) >= 3, (name, r)
