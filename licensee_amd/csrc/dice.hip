@@ -320,7 +320,8 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
     void* plan[] = {c->d_lrec, c->d_lep,  c->d_les,  c->d_lwt,   c->d_pdmt, c->d_prow,  c->d_povf, c->d_pdm,
-                    c->d_ptc,  c->d_p4q8, c->d_p4tc, c->d_p4cc,  c->d_p4off, c->d_p4rec, c->d_p4slot};
+                    c->d_ptc,  c->d_p4q8, c->d_p4tc, c->d_p4cc,  c->d_p4off, c->d_p4rec, c->d_p4slot,
+                    c->d_p4q32, c->d_p4s32};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -812,11 +813,12 @@ int dice_batch_deferred(dice_batch* b, int64_t* deferred, void* stream) {
     *deferred = 0;
     if (!b->d_ndefer || !b->ctx->prune) return DICE_OK;
     DeviceGuard g(b->ctx->device);
-    uint32_t m = 0;
+    uint32_t m[2] = {0, 0};
     hipStream_t s = pick_stream(b->ctx, stream);
-    HIP_TRY(hipMemcpyAsync(&m, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(m, b->d_ndefer, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    *deferred = m;
+    // the files that reached the postings kernels: after the survivors kernel when it ran
+    *deferred = b->surv_waves ? m[1] : m[0];
     return DICE_OK;
 }
 
@@ -831,13 +833,15 @@ int dice_batch_scored_pairs(dice_batch* b, int64_t* pairs, void* stream) {
         // (the postings kernels score them all)
         DeviceGuard g(c->device);
         hipStream_t s = pick_stream(c, stream);
-        std::vector<uint32_t> h((size_t)b->prune_waves + 1);
-        HIP_TRY(hipMemcpyAsync(h.data(), b->d_nscored, (size_t)b->prune_waves * 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(h.data() + b->prune_waves, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
+        // (dice_prune4's waves, then the survivors kernel's; the files the postings kernels scored)
+        const int64_t nw = b->prune_waves + b->surv_waves;
+        std::vector<uint32_t> h((size_t)nw + 2);
+        HIP_TRY(hipMemcpyAsync(h.data(), b->d_nscored, (size_t)nw * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h.data() + nw, b->d_ndefer, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         int64_t sum = 0;
-        for (int64_t i = 0; i < b->prune_waves; ++i) sum += h[(size_t)i];
-        *pairs = sum + (int64_t)h[(size_t)b->prune_waves] * c->T;
+        for (int64_t i = 0; i < nw; ++i) sum += h[(size_t)i];
+        *pairs = sum + (int64_t)h[(size_t)nw + (b->surv_waves ? 1 : 0)] * c->T;
     }
     return DICE_OK;
 }

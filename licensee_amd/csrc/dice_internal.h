@@ -90,7 +90,8 @@ struct dice_ctx {
     bool prune = false, prune_zero_base = false;
     uint32_t prune_wf_noclamp = 0;   // |W_F| from which the bound's length term needs no clamp
     void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
-         *d_p4slot = nullptr;
+         *d_p4slot = nullptr, *d_p4q32 = nullptr, *d_p4s32 = nullptr;
+    int32_t prune_surv_evals = 0;    // survivors kernel: exact scores per file before the postings kernels (0: off)
     int32_t p4_zkeep[2] = {-1, -1}, p4_zpos[2] = {0, 0};
     int32_t n_cu = 256, prune_max_evals = 8, prune_route = 16;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
@@ -170,11 +171,12 @@ struct dice_batch {
     size_t pdense_bytes = 0;
     size_t stage_bytes = 0;
     // pruned match (dice_prune.hip): files deferred to the postings kernels
-    int32_t* d_defer = nullptr;     // [capacity] file indices
-    uint32_t* d_ndefer = nullptr;   // count
+    int32_t* d_defer = nullptr;     // [2][capacity] file indices: dice_prune4's deferred files, the survivors kernel's
+    uint32_t* d_ndefer = nullptr;   // [2] their counts
     uint32_t* d_qctr = nullptr;     // sparse-program tile-queue counters (DICE_PROG_QUEUE A/B)
     uint32_t* d_nscored = nullptr;  // per wave of the last pruned launch: (file, template) pairs scored exactly
     int64_t prune_waves = 0;        // waves of that launch (entries of d_nscored)
+    int64_t surv_waves = 0;         // waves of the survivors kernel after it (the next entries)
     int32_t last_match = 0;         // last match call: 0 none, 1 every pair scored, 2 bound-pruned
     // Exact matcher (dice_batch_exact, lazily allocated): per-file result, field masks
     int32_t* d_exact = nullptr;

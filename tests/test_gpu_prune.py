@@ -86,8 +86,12 @@ def test_config3_files(config3, monkeypatch):
     assert 0.3 < np.mean(best >= 0) < 0.9   # the workload matches some files, not all
 
 
+# (DICE_PRUNE_SURVIVORS: exact scores per deferred file in the 32-group survivors kernel before
+# the postings kernels take it; 0, the default = no survivors kernel)
 KNOBS = [{}, {'DICE_PRUNE_MAX_EVALS': '1'}, {'DICE_PRUNE_MAX_EVALS': '0'}, {'DICE_PRUNE_ROUTE': '0'},
-         {'DICE_PRUNE_ROUTE_AT': '1'}, {'DICE_PRUNE_ROUTE': '600', 'DICE_PRUNE_ROUTE_AT': '4'}]
+         {'DICE_PRUNE_ROUTE_AT': '1'}, {'DICE_PRUNE_ROUTE': '600', 'DICE_PRUNE_ROUTE_AT': '4'},
+         {'DICE_PRUNE_SURVIVORS': '32'}, {'DICE_PRUNE_MAX_EVALS': '1', 'DICE_PRUNE_SURVIVORS': '1'},
+         {'DICE_PRUNE_ROUTE': '0', 'DICE_PRUNE_SURVIVORS': '3'}]
 
 
 @pytest.mark.parametrize('knob', range(len(KNOBS)))
@@ -124,12 +128,14 @@ def _random_files(c, n, seed, density):
     return FileBatch(bits, wf, ln, cc)
 
 
-@pytest.mark.parametrize('max_evals', ['8', '0', '1'])
-def test_files_resembling_nothing(config3, max_evals, monkeypatch):
+@pytest.mark.parametrize('max_evals,survivors', [('8', '0'), ('0', '0'), ('1', '0'), ('1', '32'), ('8', '32'), ('1', '2')])
+def test_files_resembling_nothing(config3, max_evals, survivors, monkeypatch):
     """Loose bounds: with deferral (DICE_PRUNE_MAX_EVALS, default 8; 1 defers every file that
-    needs a second exact score) those files are gathered and scored by the postings kernels;
-    0 scores them all in the pruned kernel."""
+    needs a second exact score) those files are gathered and scored by the postings kernels --
+    with DICE_PRUNE_SURVIVORS=n (A/B) first bounded again with 32 word groups and scored by the
+    survivors kernel (n exact scores at most); 0 scores them all in the pruned kernel."""
     monkeypatch.setenv('DICE_PRUNE_MAX_EVALS', max_evals)
+    monkeypatch.setenv('DICE_PRUNE_SURVIVORS', survivors)
     c, _ = config3
     fb = _random_files(c, 1500, seed=3, density=0.05)
     _check(c, fb, monkeypatch)
@@ -145,6 +151,9 @@ def test_dense_files(config3, monkeypatch):
                        for g in range(16)], 1)
     assert np.any(groups.max(1) > 255) and np.any(groups.max(1) <= 255)
     _check(c, fb, monkeypatch, thresholds=(98.0, 0.0))
+    # every file through the survivors kernel (deferred after one exact score): its 32 groups
+    # overflow a byte on the densest files (the coarse-bound path there too)
+    _check(c, fb, monkeypatch, thresholds=(98.0, 0.0), env={'DICE_PRUNE_MAX_EVALS': '1', 'DICE_PRUNE_SURVIVORS': '32'})
 
 
 def test_slow_envelope_files(config3, monkeypatch):

@@ -1,5 +1,14 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py tests/test_gpu_confidence.py -x -q --timeout 300 -m gpu > gpurun_out/t_d20.log 2>&1; echo d20_tests=$?; tail -3 gpurun_out/t_d20.log
-bash tools/gpu_ab.sh 2 "--config 3 --steps 10" DICE_POST_PRUNE=0,DICE_POST_DENSE=16 DICE_POST_PRUNE=0
-bash tools/gpu_ab.sh 2 "--config 5-T600 --steps 10" DICE_POST_DENSE=16 base
+mkdir -p gpurun_out/surv
+for e in base 16 4; do
+  if [ $e = base ]; then ENV=""; else ENV="DICE_PRUNE_SURVIVORS=$e"; fi
+  env $ENV timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/surv/$e -o run --output-format csv -- python bench.py --config 3 --steps 10 --warmup 2 --match-mode top1 --no-cpu-baseline --no-extras --extra-configs= > gpurun_out/surv/$e.json 2> gpurun_out/surv/$e.err || exit 3
+done
+python - <<'PY'
+import csv, glob
+for e in ('base', '16', '4'):
+    f = glob.glob(f'gpurun_out/surv/{e}/**/run_kernel_stats.csv', recursive=True)
+    print(e)
+    for r in csv.DictReader(open(f[0])):
+        print('  ', r['Name'][:60], r['Calls'], r['AverageNs'])
+PY
