@@ -78,6 +78,27 @@ struct Partials {
 #define POST_WALK_SINK 1
 #endif
 constexpr int kPostWaves = 16;
+// Waves per workgroup of the narrow kernels: the match kernel 16 (two workgroups per CU, 8 waves
+// per SIMD); the matrix kernel 8 at 6 waves per SIMD (three workgroups fit a CU's LDS; 5-T600
+// 5.17 -> 5.09 ms, 2 interleaved reps; the match kernel measured 3.54 -> 3.60 ms that way)
+#ifndef POST_NARROW_WAVES
+#define POST_NARROW_WAVES 16
+#endif
+#ifndef POST_NARROW_OCC
+#define POST_NARROW_OCC 8
+#endif
+#ifndef POST_MATRIX_WAVES
+#define POST_MATRIX_WAVES 8
+#endif
+// matrix kernel A/B: the next file's partials and first word chunks loaded before this file's row
+// stores, so their waits do not include the stores (1), or at the file's start (0, default): 1
+// measured 5.45 vs 5.10 ms on 5-T600 (2 interleaved reps; 80 VGPRs, the chunks live across the
+// scoring)
+#ifndef POST_MATRIX_PREFETCH
+#define POST_MATRIX_PREFETCH 0
+#endif
+template <bool kMatrix>
+constexpr int narrow_waves() { return kMatrix ? POST_MATRIX_WAVES : POST_NARROW_WAVES; }
 constexpr int kPostFiles = 64;           // files per workgroup (one tile)
 constexpr int kPostMaxTpad = 704;        // LDS budget of the dense stage (T <= 704)
 constexpr int kPostMaxDense = 16;        // dense prefix u64 words (20 / 24 measured slower at T = 600)
@@ -645,20 +666,26 @@ __device__ __forceinline__ void queue_chunks(const uint64_t (&xs)[kChunks], int3
 // here, before its first word chunks, and copied in once those are requested -- instead of being
 // prefetched into registers during the previous file's scoring, where the matrix kernel cannot
 // afford them.
-template <int WCAP, bool LATE, int PJ, int kChunks = LATE ? POST_CHUNKS_MATRIX : POST_CHUNKS_MATCH>
+template <int WCAP, bool LATE, int PJ, int kChunks = LATE ? POST_CHUNKS_MATRIX : POST_CHUNKS_MATCH, bool PF = false>
 __device__ __forceinline__ void file_postings(const uint64_t* __restrict__ row, int32_t w64, int32_t pb0,
                                               const Partials& pt, int64_t pos, bool wide, int32_t tp, uint32_t* wq,
                                               uint2* lq,
                                               const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
-                                              uint32_t* crow32, int lane) {
+                                              uint32_t* crow32, int lane, const uint64_t (*xs0)[kChunks] = nullptr) {
     uint32_t nq = 0;           // queued narrow words (wave-uniform)
     uint32_t nl = 0;           // queued long words (uniform)
     // queue the file's narrow words (set bits of u64 words >= D), kChunks x 64 words loaded
     // together (queue_chunks). The first round is peeled so that LATE's partials are copied in
-    // between its loads and their use and are dead for the rest of the file.
+    // between its loads and their use and are dead for the rest of the file; with PF the first
+    // round arrives prefetched (xs0: loaded before the previous file was scored).
     int32_t pb = pb0;
     uint64_t xs[kChunks];
-    if (LATE) {
+    if (PF) {
+        if (pb < w64) {
+            queue_chunks<WCAP, kChunks>(*xs0, pb, wq, nq, lq, nl, prow, plong, crow32, lane);
+            pb += kChunks * kWave;
+        }
+    } else if (LATE) {
         uint32_t part[PJ];
         load_partials<PJ, true>(pt, pos, tp, wide, lane, part);
         if (pb < w64) load_chunks<kChunks>(row, w64, pb, lane, xs);
@@ -905,24 +932,25 @@ __device__ __forceinline__ void post_narrow_body(
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
+    constexpr int kNarrowWaves = narrow_waves<kMatrix>();
     constexpr int kTJ = (TPMAX + kWave - 1) / kWave;           // templates per lane
     constexpr int kWCap = word_cap<TPMAX>();
     constexpr int kPJ = pairs_per_lane<TPMAX>();
     // u32 counters, one row per wave, then the queues of narrow word ids: one array, so the queue
     // slots (the walk's sinks, count_or_sink) lie past every counter row and within 64 KiB of it
-    __shared__ uint32_t cntq[kPostWaves * TPMAX + kPostWaves * kWCap];
+    __shared__ uint32_t cntq[kNarrowWaves * TPMAX + kNarrowWaves * kWCap];
     // (wave w's sinks end 4 (16 TPMAX + (w + 1) WCAP) bytes in, its row starts at 4 w TPMAX: the
     // largest gap is wave 0's)
-    static_assert(kWCap <= TPMAX && (kPostWaves * TPMAX + kWCap) * 4 <= 0xFFFE, "sinks within reach of every row");
+    static_assert(kWCap <= TPMAX && (kNarrowWaves * TPMAX + kWCap) * 4 <= 0xFFFE, "sinks within reach of every row");
     uint32_t* const cnt32 = cntq;
-    uint32_t (*const wq)[kWCap] = reinterpret_cast<uint32_t (*)[kWCap]>(cntq + kPostWaves * TPMAX);
+    uint32_t (*const wq)[kWCap] = reinterpret_cast<uint32_t (*)[kWCap]>(cntq + kNarrowWaves * TPMAX);
     __shared__ uint2 tcs[TPMAX];                               // packed template constants
-    __shared__ uint2 lq[kPostWaves][kLongCap];                 // queued long words (offset, length)
-    __shared__ uint2 tsc[kMatrix ? kPostWaves : 1][kPostFiles / kPostWaves];   // matrix: own files' {|W_F|, len_F}
+    __shared__ uint2 lq[kNarrowWaves][kLongCap];                 // queued long words (offset, length)
+    __shared__ uint2 tsc[kMatrix ? kNarrowWaves : 1][kPostFiles / kNarrowWaves];   // matrix: own files' {|W_F|, len_F}
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     uint32_t* crow32 = cnt32 + wave * TPMAX;
-    for (int i = threadIdx.x; i < T; i += kPostWaves * kWave) tcs[i] = tc[i];
+    for (int i = threadIdx.x; i < T; i += kNarrowWaves * kWave) tcs[i] = tc[i];
     for (int i = lane; i < TPMAX; i += kWave) crow32[i] = 0;
     __syncthreads();
 
@@ -950,15 +978,21 @@ __device__ __forceinline__ void post_narrow_body(
         // VGPRs live across the whole tile (the scoring's registers need them)
         uint32_t lw = (uint32_t)lane;
         asm volatile("" : "+v"(lw));   // the slot address formed here, not hoisted out of the tile loop
-        if ((lw & (kPostWaves - 1)) == (uint32_t)wave) tsc[wave][lw >> 4] = make_uint2(twf, tlen);
+        if ((lw & (kNarrowWaves - 1)) == (uint32_t)wave) tsc[wave][lw / kNarrowWaves] = make_uint2(twf, tlen);
     }
     // the tile's partial formats (bit l: position f0 + l has a u16 row)
     const uint64_t tov = POST_PARTIALS_U8 ? __ballot(pt.flag[f0 + min(lane, nt - 1)] != 0) : ~0ull;
     // match mode: the next file's dense partials, prefetched while the wave scores the previous
-    // file (the matrix kernel loads them at the file's start: file_postings LATE)
+    // file (the matrix kernel loads them at the file's start: file_postings LATE); matrix mode with
+    // POST_MATRIX_PREFETCH: the next file's partials and first word chunks, loaded before this
+    // file's row stores -- so their waits do not wait for the stores (gfx950's vmcnt counts stores)
+    constexpr bool kPF = kMatrix && POST_MATRIX_PREFETCH && TPMAX <= 608;   // (704-template rows: no VGPRs left)
+    constexpr int kNC = kMatrix ? POST_CHUNKS_MATRIX : POST_CHUNKS_MATCH;
     uint32_t pre[kPJ];
-    if (!kMatrix && wave < nt) load_partials<kPJ, false>(pt, f0 + wave, tp, (tov >> wave) & 1, lane, pre);
-    for (int fi = wave; fi < kPostFiles; fi += kPostWaves) {
+    uint64_t xs0[kPF ? kNC : 1];
+    if ((!kMatrix || kPF) && wave < nt) load_partials<kPJ, false>(pt, f0 + wave, tp, (tov >> wave) & 1, lane, pre);
+    if (kPF && wave < nt && pb0 < w64) load_chunks<kNC>(rows + (f0 + wave) * w64, w64, pb0, lane, *reinterpret_cast<uint64_t (*)[kNC]>(xs0));
+    for (int fi = wave; fi < kPostFiles; fi += kNarrowWaves) {
         const int64_t pos = f0 + fi;
         if (fi >= nt) break;   // wave-uniform
         const int64_t file = idx ? (int64_t)rfl(__builtin_amdgcn_readlane(tfile, fi)) : pos;
@@ -969,13 +1003,14 @@ __device__ __forceinline__ void post_narrow_body(
         int32_t Tf = T, tpf = tp, ldf = ld;
         int lanef = lane;   // likewise every lane-derived constant (lane + 64 j, lane addresses)
         if (kMatrix) asm volatile("" : "+s"(Tf), "+s"(tpf), "+s"(ldf), "+v"(lanef));
-        // this file's dense partials start its counter row (matrix mode: inside file_postings)
+        // this file's dense partials start its counter row (matrix mode without prefetch: inside
+        // file_postings)
         const bool wide = (tov >> fi) & 1;
-        if (!kMatrix) copy_in<kPJ>(crow32, pre, tpf, wide, lanef);
+        if (!kMatrix || kPF) copy_in<kPJ>(crow32, pre, tpf, wide, lanef);
         uint32_t wf;
         int32_t lf;
         if (kMatrix) {
-            const uint2 sc = tsc[wave][fi >> 4];   // uniform address: a broadcast read
+            const uint2 sc = tsc[wave][fi / kNarrowWaves];   // uniform address: a broadcast read
             wf = rfl(sc.x);
             lf = (int32_t)rfl(sc.y);
         } else {
@@ -983,11 +1018,19 @@ __device__ __forceinline__ void post_narrow_body(
             lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
         }
         const bool cc = ((tcc >> fi) & 1u) != 0;
-        file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow, plong, crow32,
-                                           lanef);
-        // match mode: the wave's next file's partials fly while this one is scored
-        if (!kMatrix && fi + kPostWaves < nt)
-            load_partials<kPJ, false>(pt, pos + kPostWaves, tpf, (tov >> (fi + kPostWaves)) & 1, lane, pre);
+        if (kPF) {
+            file_postings<kWCap, true, kPJ, kNC, true>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow,
+                                                       plong, crow32, lanef,
+                                                       reinterpret_cast<const uint64_t (*)[kNC]>(xs0));
+        } else {
+            file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow, plong,
+                                               crow32, lanef);
+        }
+        // the wave's next file's partials (and with kPF its first chunks) fly while this one is scored
+        if ((!kMatrix || kPF) && fi + kNarrowWaves < nt)
+            load_partials<kPJ, false>(pt, pos + kNarrowWaves, tpf, (tov >> (fi + kNarrowWaves)) & 1, lane, pre);
+        if (kPF && fi + kNarrowWaves < nt && pb0 < w64)
+            load_chunks<kNC>(rows + (pos + kNarrowWaves) * w64, w64, pb0, lane, *reinterpret_cast<uint64_t (*)[kNC]>(xs0));
 
         if (POST_DIAG & 8) continue;
         score_file<kMatrix, KM, kTJ>(crow32, tcs, Tf, ldf, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
@@ -999,7 +1042,7 @@ __device__ __forceinline__ void post_narrow_body(
 // Match mode held to 64 VGPRs (8 waves per SIMD: two workgroups per CU); the matrix mode's
 // top-k slots need more registers and run at the occupancy they get.
 template <int TPMAX>
-__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void dice_post_narrow_match(
+__global__ __launch_bounds__(narrow_waves<false>() * kWave) __attribute__((amdgpu_waves_per_eu(POST_NARROW_OCC, POST_NARROW_OCC))) void dice_post_narrow_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
@@ -1011,13 +1054,14 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
                                score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
-// POST_MATRIX_OCC (A/B): waves per SIMD the matrix kernel is compiled for (8: two workgroups
+// POST_MATRIX_OCC (A/B): waves per SIMD the matrix kernel is compiled for (6 with its 8-wave
+// workgroups: three per CU; 8 with 16-wave workgroups: two workgroups
 // per CU as in match mode, at 64 VGPRs)
 #ifndef POST_MATRIX_OCC
-#define POST_MATRIX_OCC 8
+#define POST_MATRIX_OCC 6
 #endif
 template <int KM, int TPMAX>
-__global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per_eu(POST_MATRIX_OCC, POST_MATRIX_OCC))) void dice_post_narrow_matrix(
+__global__ __launch_bounds__(narrow_waves<true>() * kWave) __attribute__((amdgpu_waves_per_eu(POST_MATRIX_OCC, POST_MATRIX_OCC))) void dice_post_narrow_matrix(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
     const uint2* __restrict__ tc, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
@@ -1239,7 +1283,9 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     if (rc) return rc;
     const int64_t tiles = (b->n + kPostFiles - 1) / kPostFiles;
     // two workgroups per CU are resident in either kernel (LDS)
-    const int64_t groups = idx ? std::min<int64_t>(tiles, 2 * (int64_t)c->n_cu) : tiles;
+    // (the narrow kernel's workgroups resident per CU: two 16-wave, three 8-wave)
+    constexpr int kNarrowWaves = narrow_waves<kMatrix>();
+    const int64_t groups = idx ? std::min<int64_t>(tiles, (kNarrowWaves == 16 ? 2 : 3) * (int64_t)c->n_cu) : tiles;
     const Partials pt = partials_of(c, b);
     if (c->post_dense == 0 || (POST_DIAG & 1)) {
         // no dense prefix: zero partials (u8 rows with flags 0; u16 rows when every row is u16)
@@ -1260,7 +1306,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     }
     auto kern = c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608> : dice_post_narrow_match<608>)
                                   : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad> : dice_post_narrow_match<kPostMaxTpad>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kNarrowWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        pt, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,

@@ -27,12 +27,14 @@ def _resources(src):
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
 def test_postings_kernels_fit_8_waves_without_scratch():
     res = _resources('dice_post.hip')
-    for name in ('dice_post_narrow_match<608>', 'dice_post_narrow_matrix<1, 608>', 'dice_post_dense<16, 608>',
-                 'dice_post_narrow_match<704>', 'dice_post_narrow_matrix<1, 704>'):
+    # (the matrix kernels run 8-wave workgroups at 6 waves per SIMD: three per CU)
+    for name, occ in (('dice_post_narrow_match<608>', 8), ('dice_post_narrow_matrix<1, 608>', 6),
+                      ('dice_post_dense<16, 608>', 8), ('dice_post_narrow_match<704>', 8),
+                      ('dice_post_narrow_matrix<1, 704>', 6)):
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0', (name, r)
         assert r['VGPRs Spill'] == '0', (name, r)
-        assert int(r['Occupancy [waves/SIMD]']) == 8, (name, r)
+        assert int(r['Occupancy [waves/SIMD]']) == occ, (name, r)
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')

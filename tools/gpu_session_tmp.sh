@@ -1,14 +1,4 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out/surv
-for e in base 16 4; do
-  if [ $e = base ]; then ENV=""; else ENV="DICE_PRUNE_SURVIVORS=$e"; fi
-  env $ENV timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/surv/$e -o run --output-format csv -- python bench.py --config 3 --steps 10 --warmup 2 --match-mode top1 --no-cpu-baseline --no-extras --extra-configs= > gpurun_out/surv/$e.json 2> gpurun_out/surv/$e.err || exit 3
-done
-python - <<'PY'
-import csv, glob
-for e in ('base', '16', '4'):
-    f = glob.glob(f'gpurun_out/surv/{e}/**/run_kernel_stats.csv', recursive=True)
-    print(e)
-    for r in csv.DictReader(open(f[0])):
-        print('  ', r['Name'][:60], r['Calls'], r['AverageNs'])
-PY
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py -k "post or slow" -x -q --timeout 300 -m gpu > gpurun_out/t_pf.log 2>&1; echo pf_tests=$?; tail -2 gpurun_out/t_pf.log
+bash tools/gpu_ab.sh 2 "--config 5-T600 --steps 10" base lib:nopf lib:m16o8
