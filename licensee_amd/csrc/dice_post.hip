@@ -377,6 +377,17 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 // tile is scored (LDS waits count lgkmcnt, so they fly across the tile) and written to LDS after
 // it. (5-T600 dense kernel, step by step: 1.70 ms -> 0.68 ms, the VALU kernel 1.45;
 // profiles/r4_mfma_dense.txt.)
+// timing splits only (tools/build_variant.sh -DPOST_DENSE_AB=n; results wrong): 1 = no partial
+// stores, 2 = no k-loop, 3 = no store phase (no slab, no stores)
+#ifndef POST_DENSE_AB
+#define POST_DENSE_AB 0
+#endif
+#ifndef POST_DENSE_PLANES
+#define POST_DENSE_PLANES 1   // FP4: u32 planes in LDS and shift-free widening (widen_a / widen_b)
+#endif
+#ifndef POST_DENSE_WIDE
+#define POST_DENSE_WIDE 1   // 128-byte row pieces from waves with two N-tiles (0: 64-byte pieces)
+#endif
 constexpr int kMfmaNT = 2;       // N-tiles per wave (at most)
 constexpr int kSlabStride = 40;  // u16 per slab row (one 32-template N-tile + 8): rows 4 apart 16 banks apart
 constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>= 11 waves x 2 N-tiles x 32)
@@ -419,6 +430,36 @@ __device__ __forceinline__ v8i widen_nibbles(uint32_t v) {
     return r;
 }
 constexpr int kE8M0Two = 0x80808080;   // block scale 2^1 in every byte
+constexpr int kE8M0One = 0x7F7F7F7F;   // block scale 2^0
+
+// The planes form (POST_DENSE_PLANES, default 1): nibble i of fragment dword k still holds bit
+// 4 i + k of the word, but left where a mask finds it, so the two operands carry different e2m1
+// values per dword and each product is still exactly 1.0 at block scales 2^0:
+//   dword   A (file prefix)          value   B (template mask)          value
+//   0       v & 0x11111111           0.5     (v << 2) & 0x44444444      2.0
+//   1       v & 0x22222222           1.0     v & 0x22222222             1.0
+//   2       v & 0x44444444           2.0     (v >> 2) & 0x11111111      0.5
+//   3       (v >> 1) & 0x44444444    2.0     (v >> 3) & 0x11111111      0.5
+// (e2m1 0b0001 = 0.5, 0b0010 = 1.0, 0b0100 = 2.0): 5 VALU for A, 7 for B (8 each before), and A
+// is widened MT times per word.
+__device__ __forceinline__ v8i widen_a(uint32_t v) {
+    v8i r;
+    r[0] = (int)(v & 0x11111111u);
+    r[1] = (int)(v & 0x22222222u);
+    r[2] = (int)(v & 0x44444444u);
+    r[3] = (int)((v >> 1) & 0x44444444u);
+    r[4] = r[5] = r[6] = r[7] = 0;
+    return r;
+}
+__device__ __forceinline__ v8i widen_b(uint32_t v) {
+    v8i r;
+    r[0] = (int)((v << 2) & 0x44444444u);
+    r[1] = (int)(v & 0x22222222u);
+    r[2] = (int)((v >> 2) & 0x11111111u);
+    r[3] = (int)((v >> 3) & 0x11111111u);
+    r[4] = r[5] = r[6] = r[7] = 0;
+    return r;
+}
 
 // A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one (M-tile,
 // N-tile) at a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as
@@ -430,6 +471,40 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][NTW], uint1
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
     const int32_t rf = lf & 31, hf = lf >> 5;
+    if constexpr (NTW == 2 && POST_DENSE_WIDE) {
+        if (te - tb == 64) {   // uniform: a wave with two N-tiles stores 128-byte row pieces
+            // per (M-tile, half s): files 16 s .. 16 s + 15 (accumulator registers 8 s .. 8 s + 7) x the
+            // wave's 64 templates through a 16 x 64 slab (rows 128 B, unpadded: the b16 writes of one
+            // row and the b128 reads of 8 rows x 128 B are bank-conflict free), then each store
+            // instruction writes 8 whole 128-byte row pieces
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+#pragma unroll
+                for (int sh = 0; sh < 2; ++sh) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int gg = 0; gg < 8; ++gg) {
+                            const int g = 8 * sh + gg;
+                            slab[((g & 3) + 8 * ((g >> 2) & 1) + 4 * hf) * 64 + 32 * j + rf] =
+                                (uint16_t)(uint32_t)acc[m][j][g];
+                        }
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int row = (lf >> 3) + 8 * i, piece = lf & 7;
+                        const uint4 v = *reinterpret_cast<const uint4*>(slab + row * 64 + piece * 8);
+                        const int64_t file = f0 + 32 * m + 16 * sh + row;
+                        const int32_t t = tb + piece * 8;
+                        if (POST_DENSE_AB != 1 && t < tpf && file < nn)
+                            *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
 #pragma unroll
@@ -445,7 +520,7 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][NTW], uint1
                 const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
                 const int64_t file = f0 + 32 * m + row;
                 const int32_t t = tb + 32 * j + piece * 8;
-                if (t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+                if (POST_DENSE_AB != 1 && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -497,19 +572,37 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const int i = (int)threadIdx.x + k * NW * kWave;
-            if (i < kPreWords) pre[buf][(i / DP) * kPreStride + i % DP] = pv[k];
+            if (i < kPreWords) {
+                const int at = (i / DP) * kPreStride + i % DP;
+                if constexpr (F4 && POST_DENSE_PLANES) {   // low and high dwords in two planes
+                    uint32_t* p32 = reinterpret_cast<uint32_t*>(pre[buf]);
+                    p32[at] = (uint32_t)pv[k];
+                    p32[kTF * kPreStride + at] = (uint32_t)(pv[k] >> 32);
+                } else {
+                    pre[buf][at] = pv[k];
+                }
+            }
         }
     };
     // the masks once per (persistent) workgroup: LDS reads in the k-loop wait on lgkmcnt, so the
     // next tile's prefix loads (vmcnt) fly across the whole tile
-    for (int i = threadIdx.x; i < DP * kCols; i += NW * kWave) bm[i] = dmask[(i / kCols) * kMfmaCols + i % kCols];
+    for (int i = threadIdx.x; i < DP * kCols; i += NW * kWave) {
+        const uint64_t v = dmask[(i / kCols) * kMfmaCols + i % kCols];
+        if constexpr (F4 && POST_DENSE_PLANES) {
+            reinterpret_cast<uint32_t*>(bm)[i] = (uint32_t)v;
+            reinterpret_cast<uint32_t*>(bm)[DP * kCols + i] = (uint32_t)(v >> 32);
+        } else {
+            bm[i] = v;
+        }
+    }
     uint64_t pv[kPer];
     load_pre(f0, pv);
     store_pre(0, pv);
     __syncthreads();
     for (int buf = 0; f0 < nn; f0 += stride, buf = (buf + 1) % kBufs) {
-        const bool more = f0 + stride < nn;   // uniform
-        if (more) load_pre(f0 + stride, pv);
+        // unconditional (zeros past the end): a load under `if (more)` left pending on the skip path
+        // would make the loop head wait vmcnt(0) for this tile's stores
+        load_pre(f0 + stride, pv);
         using Acc = typename std::conditional<F4, v16f, v16i>::type;
         Acc acc[MT][NTW];
 #pragma unroll
@@ -519,14 +612,37 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
         const uint64_t* pb = pre[buf];
         const uint64_t* bcol = bm + tb + r;
 #pragma unroll 2
-        for (int q = 0; q < DP; ++q) {
-            uint64_t bw[NTW];
+        for (int q = 0; q < (POST_DENSE_AB == 2 ? 0 : DP); ++q) {
+            uint64_t bw[NTW] = {}, a[MT] = {};
+            if constexpr (!(F4 && POST_DENSE_PLANES)) {
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) bw[j] = j < nw_tiles ? bcol[q * kCols + j * 32] : 0;   // (uniform: no read past bm)
-            uint64_t a[MT];
+                for (int j = 0; j < NTW; ++j) bw[j] = j < nw_tiles ? bcol[q * kCols + j * 32] : 0;   // (uniform: no read past bm)
 #pragma unroll
-            for (int m = 0; m < MT; ++m) a[m] = pb[(32 * m + r) * kPreStride + q];
-            if constexpr (F4) {
+                for (int m = 0; m < MT; ++m) a[m] = pb[(32 * m + r) * kPreStride + q];
+            }
+            if constexpr (F4 && POST_DENSE_PLANES) {
+                // lane half h reads its dwords from plane h (no 64-bit shift; conflict-free b32 reads:
+                // the prefix rows' stride is odd) and widens them without shifts where the nibble
+                // class allows (widen_a / widen_b: products 1.0 at block scales 2^0)
+                const uint32_t* pa = reinterpret_cast<const uint32_t*>(pb) + h * (kTF * kPreStride) + r * kPreStride + q;
+                const uint32_t* pw = reinterpret_cast<const uint32_t*>(bm) + h * (DP * kCols) + q * kCols + tb + r;
+                uint32_t bw32[NTW];
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) bw32[j] = j < nw_tiles ? pw[j * 32] : 0;
+                v8i fa[MT];
+#pragma unroll
+                for (int m = 0; m < MT; ++m) fa[m] = widen_a(pa[32 * m * kPreStride]);
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) {
+                    if (j < nw_tiles) {   // uniform
+                        const v8i fb = widen_b(bw32[j]);
+#pragma unroll
+                        for (int m = 0; m < MT; ++m)
+                            acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[m], fb, acc[m][j], 4, 4, 0,
+                                                                                         kE8M0One, 0, kE8M0One);
+                    }
+                }
+            } else if constexpr (F4) {
                 // one instruction per (M-tile, N-tile) and word: lane half h holds bits [32 h, 32 h + 32)
                 v8i fa[MT];
 #pragma unroll
@@ -560,8 +676,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             }
         }
         if (kBufs == 1) __syncthreads();   // every wave is done with the one prefix buffer
-        mfma_store_tile<NTW, MT>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
-        if (more) store_pre((buf + 1) % kBufs, pv);
+        // the next tile's prefixes into LDS before this tile's stores are issued: the wait on their
+        // loads (vmcnt counts stores too, in order) then finds only the previous tile's stores,
+        // issued a whole k-loop ago, and this tile's stores drain under the next tile's MFMAs
+        store_pre((buf + 1) % kBufs, pv);
+        if (POST_DENSE_AB != 3) mfma_store_tile<NTW, MT>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
         __syncthreads();   // the next tile's prefixes are complete (MT = 2: the other buffer)
     }
 }

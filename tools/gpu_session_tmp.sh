@@ -1,3 +1,14 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/gpu_ab.sh 2 "--config 3 --steps 10" DICE_POST_PRUNE=0 lib:qu1,DICE_POST_PRUNE=0 lib:qu4,DICE_POST_PRUNE=0 DICE_POST_PRUNE=0,DICE_POST_MFMA_MT=2
+timeout -k 10 600 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py tests/test_gpu_prune.py tests/test_gpu_parity.py -x -q --timeout 300 -m gpu > gpurun_out/t_post.log 2>&1 || { echo tests failed; tail -30 gpurun_out/t_post.log; exit 3; }
+tail -2 gpurun_out/t_post.log
+for v in base noplanes kloop_only head; do
+  unset LICENSEE_DICE_LIB
+  [ $v != base ] && export LICENSEE_DICE_LIB=licensee_amd/lib/var/$v.so
+  rm -rf gpurun_out/split_$v
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/split_$v -o run -- python bench.py --config 5-T600 --steps 10 --warmup 2 --extra-configs= --no-cpu-baseline --no-extras > gpurun_out/split_$v.json 2> gpurun_out/split_$v.err || { echo "$v failed"; exit 3; }
+  echo "== $v"; python tools/rocpd_summary.py gpurun_out/split_$v/run_results.db --match dice_post
+done
+unset LICENSEE_DICE_LIB
+bash tools/gpu_ab.sh 3 "--config 5-T600 --steps 10" base lib:noplanes lib:head
+bash tools/gpu_ab.sh 3 "--config 3 --steps 10" DICE_POST_PRUNE=0 lib:noplanes,DICE_POST_PRUNE=0 lib:head,DICE_POST_PRUNE=0
