@@ -382,14 +382,16 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
 #ifndef POST_DENSE_AB
 #define POST_DENSE_AB 0
 #endif
+#ifndef POST_DENSE_BIAS
+// FP4 planes: accumulators start at 2^23 so the counts sit in the low bits of their encodings (no
+// cvt) -- off: parity failed at T = 65, the scaled FP4 MFMA does not add 64 unit products to 2^23
+// exactly (its accumulation is not a full-precision f32 add; from 0 the counts stay exact)
+#define POST_DENSE_BIAS 0
+#endif
 #ifndef POST_DENSE_PLANES
 #define POST_DENSE_PLANES 1   // FP4: u32 planes in LDS and shift-free widening (widen_a / widen_b)
 #endif
-#ifndef POST_DENSE_WIDE
-#define POST_DENSE_WIDE 1   // 128-byte row pieces from waves with two N-tiles (0: 64-byte pieces)
-#endif
 constexpr int kMfmaNT = 2;       // N-tiles per wave (at most)
-constexpr int kSlabStride = 40;  // u16 per slab row (one 32-template N-tile + 8): rows 4 apart 16 banks apart
 constexpr int kMfmaCols = 768;   // template columns of the word-major masks (>= 11 waves x 2 N-tiles x 32)
 constexpr int kMfmaMaxDense = 20;   // prefix u64 words of the matrix-core kernels (the masks' LDS budget)
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -461,65 +463,57 @@ __device__ __forceinline__ v8i widen_b(uint32_t v) {
     return r;
 }
 
-// A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one (M-tile,
-// N-tile) at a time: in as u16 (file row, template column), back as 16-byte row pieces, stored as
-// 64-byte runs of the rows (2-byte stores straight from the accumulators: 1.04 ms vs 0.94; a
-// 64-template slab per M-tile needed twice the LDS, which the 20-word masks now use).
-template <int NTW, int MT, class ACC>
-__device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][NTW], uint16_t* slab, uint16_t* __restrict__ part,
+// A tile's accumulators out to the [n][tp] u16 partials through the wave's LDS slab, one piece =
+// (M-tile m, 16-file half sh: accumulator registers 8 sh .. 8 sh + 7) at a time: in as u16 (file
+// row, template column) into a 16 x 64 slab (rows 128 B, unpadded: the b16 writes of one row are
+// conflict-free), back as 16-byte row pieces. A wave with two N-tiles then stores 8 whole 128-byte
+// row pieces per instruction (the b128 reads of 8 rows x 128 B are conflict-free); a wave with one
+// stores 16 rows x 64 bytes (2-way conflicts on that one read). (2-byte stores straight from the
+// accumulators: 1.04 ms vs 0.94; 64-byte pieces from a 32 x 32 slab: 549 vs 528 us, 5-T600.)
+// BIASED: the accumulators started at 2^23 (dice_post_dense_mfma, FP4 planes form), so the low 16
+// bits of their f32 encodings are the counts -- no conversion.
+constexpr int kSlabCols = 64;   // u16 per slab row (one wave's two N-tiles)
+template <int MT, bool BIASED, class ACC>
+__device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_t* slab, uint16_t* __restrict__ part,
                                                 int64_t f0, int64_t nn, int32_t tb, int32_t te, int32_t tp, int lane) {
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
     const int32_t rf = lf & 31, hf = lf >> 5;
-    if constexpr (NTW == 2 && POST_DENSE_WIDE) {
-        if (te - tb == 64) {   // uniform: a wave with two N-tiles stores 128-byte row pieces
-            // per (M-tile, half s): files 16 s .. 16 s + 15 (accumulator registers 8 s .. 8 s + 7) x the
-            // wave's 64 templates through a 16 x 64 slab (rows 128 B, unpadded: the b16 writes of one
-            // row and the b128 reads of 8 rows x 128 B are bank-conflict free), then each store
-            // instruction writes 8 whole 128-byte row pieces
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-#pragma unroll
-                for (int sh = 0; sh < 2; ++sh) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-#pragma unroll
-                        for (int gg = 0; gg < 8; ++gg) {
-                            const int g = 8 * sh + gg;
-                            slab[((g & 3) + 8 * ((g >> 2) & 1) + 4 * hf) * 64 + 32 * j + rf] =
-                                (uint16_t)(uint32_t)acc[m][j][g];
-                        }
-                    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const int row = (lf >> 3) + 8 * i, piece = lf & 7;
-                        const uint4 v = *reinterpret_cast<const uint4*>(slab + row * 64 + piece * 8);
-                        const int64_t file = f0 + 32 * m + 16 * sh + row;
-                        const int32_t t = tb + piece * 8;
-                        if (POST_DENSE_AB != 1 && t < tpf && file < nn)
-                            *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            return;
-        }
-    }
+    const int32_t nt = (te - tb) / 32;   // the wave's N-tiles (uniform: 0, 1 or 2)
+    if (nt == 0) return;
+    auto val = [&](int m, int j, int g) -> uint16_t {
+        if constexpr (BIASED) return (uint16_t)__builtin_bit_cast(uint32_t, acc[m][j][g]);
+        else return (uint16_t)(uint32_t)acc[m][j][g];
+    };
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-            if (tb + 32 * j >= te) break;   // uniform: the wave's second N-tile may not exist
+        for (int sh = 0; sh < 2; ++sh) {
 #pragma unroll
-            for (int g = 0; g < 16; ++g)
-                slab[((g & 3) + 8 * (g >> 2) + 4 * hf) * kSlabStride + rf] = (uint16_t)(uint32_t)acc[m][j][g];
+            for (int j = 0; j < 2; ++j) {
+                if (j < nt) {   // uniform
+#pragma unroll
+                    for (int gg = 0; gg < 8; ++gg) {
+                        const int g = 8 * sh + gg;
+                        slab[((g & 3) + 8 * ((g >> 2) & 1) + 4 * hf) * kSlabCols + 32 * j + rf] = val(m, j, g);
+                    }
+                }
+            }
             __builtin_amdgcn_wave_barrier();
+            if (nt == 2) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int row = (lf >> 2) + 16 * i, piece = lf & 3;
-                const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabStride + piece * 8);
-                const int64_t file = f0 + 32 * m + row;
-                const int32_t t = tb + 32 * j + piece * 8;
+                for (int i = 0; i < 2; ++i) {
+                    const int row = (lf >> 3) + 8 * i, piece = lf & 7;
+                    const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabCols + piece * 8);
+                    const int64_t file = f0 + 32 * m + 16 * sh + row;
+                    const int32_t t = tb + piece * 8;
+                    if (POST_DENSE_AB != 1 && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+                }
+            } else {
+                const int row = lf >> 2, piece = lf & 3;
+                const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabCols + piece * 8);
+                const int64_t file = f0 + 32 * m + 16 * sh + row;
+                const int32_t t = tb + piece * 8;
                 if (POST_DENSE_AB != 1 && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
             }
             __builtin_amdgcn_wave_barrier();
@@ -532,20 +526,23 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
     const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
     const uint32_t* __restrict__ pn) {
-    // MT 32-file M-tiles per tile; the prefix buffer is doubled when LDS allows (MT = 2), else one
-    // buffer and a second barrier per tile
+    // MT 32-file M-tiles per tile; the prefix buffer is doubled when LDS allows (one barrier per
+    // tile; every shipped shape since the 16 x 64 slabs), else one buffer and a second barrier
     static_assert(DP <= kMfmaMaxDense, "prefix wider than the masks' table");
+    static_assert(NTW == 2, "two N-tiles per wave (the store slab)");
     constexpr int kTF = 32 * MT;                     // files per tile
-    constexpr int kBufs = MT == 2 ? 2 : 1;
     // DP + 1 u64 per file row (odd: the 32 lanes of a ds_read_b64 column read hit 64 distinct banks)
     constexpr int kPreStride = DP + 1;
     constexpr int kPreWords = kTF * DP;
     constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);   // prefix words per thread
     constexpr int kCols = NTW == 2 && NW == 12 ? 640 : NW * NTW * 32;   // the workgroup's template columns
+    constexpr size_t kFixed = (size_t)DP * kCols * 8 + (size_t)NW * 16 * kSlabCols * 2;
+    constexpr int kBufs = kFixed + 2 * (size_t)kTF * kPreStride * 8 <= 160 * 1024 ? 2 : 1;
     __shared__ uint64_t pre[kBufs][kTF * kPreStride];
     __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 110 KiB at DP 20)
-    __shared__ uint16_t tslab[NW][32 * kSlabStride];  // per-wave transpose of one 32 x 32 tile (2.5 KiB)
+    __shared__ uint16_t tslab[NW][16 * kSlabCols];   // per-wave 16 x 64 transpose slab (2 KiB)
     static_assert(sizeof(pre) + sizeof(bm) + sizeof(tslab) <= 160 * 1024, "one workgroup's LDS");
+    constexpr bool kBiased = F4 && POST_DENSE_PLANES && POST_DENSE_BIAS;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
@@ -599,20 +596,25 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     load_pre(f0, pv);
     store_pre(0, pv);
     __syncthreads();
+    v16f bias;   // 2^23: the accumulators' f32 encodings then hold the counts in their low bits
+#pragma unroll
+    for (int g = 0; g < 16; ++g) bias[g] = 8388608.0f;
     for (int buf = 0; f0 < nn; f0 += stride, buf = (buf + 1) % kBufs) {
         // unconditional (zeros past the end): a load under `if (more)` left pending on the skip path
         // would make the loop head wait vmcnt(0) for this tile's stores
         load_pre(f0 + stride, pv);
         using Acc = typename std::conditional<F4, v16f, v16i>::type;
         Acc acc[MT][NTW];
+        if constexpr (!kBiased) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
+            for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) acc[m][j] = Acc{};
+                for (int j = 0; j < NTW; ++j) acc[m][j] = Acc{};
+        }
         const uint64_t* pb = pre[buf];
         const uint64_t* bcol = bm + tb + r;
-#pragma unroll 2
-        for (int q = 0; q < (POST_DENSE_AB == 2 ? 0 : DP); ++q) {
+        // one prefix word (biased: the first word's MFMAs take C from `bias`; q = 0 is peeled)
+        auto word = [&](int q, auto first) {
             uint64_t bw[NTW] = {}, a[MT] = {};
             if constexpr (!(F4 && POST_DENSE_PLANES)) {
 #pragma unroll
@@ -638,8 +640,9 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
                         const v8i fb = widen_b(bw32[j]);
 #pragma unroll
                         for (int m = 0; m < MT; ++m)
-                            acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[m], fb, acc[m][j], 4, 4, 0,
-                                                                                         kE8M0One, 0, kE8M0One);
+                            acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                                fa[m], fb, kBiased && decltype(first)::value ? bias : acc[m][j], 4, 4, 0, kE8M0One, 0,
+                                kE8M0One);
                     }
                 }
             } else if constexpr (F4) {
@@ -674,13 +677,18 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
                 }
             }
             }
+        };
+        if (POST_DENSE_AB != 2) {
+            word(0, std::true_type{});
+#pragma unroll 2
+            for (int q = 1; q < DP; ++q) word(q, std::false_type{});
         }
         if (kBufs == 1) __syncthreads();   // every wave is done with the one prefix buffer
         // the next tile's prefixes into LDS before this tile's stores are issued: the wait on their
         // loads (vmcnt counts stores too, in order) then finds only the previous tile's stores,
         // issued a whole k-loop ago, and this tile's stores drain under the next tile's MFMAs
         store_pre((buf + 1) % kBufs, pv);
-        if (POST_DENSE_AB != 3) mfma_store_tile<NTW, MT>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
+        if (POST_DENSE_AB != 3) mfma_store_tile<MT, kBiased>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
         __syncthreads();   // the next tile's prefixes are complete (MT = 2: the other buffer)
     }
 }

@@ -2,7 +2,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py tests/test_gpu_prune.py tests/test_gpu_parity.py -x -q --timeout 300 -m gpu > gpurun_out/t_post.log 2>&1 || { echo tests failed; tail -30 gpurun_out/t_post.log; exit 3; }
 tail -2 gpurun_out/t_post.log
-for v in base noplanes kloop_only head; do
+LICENSEE_DICE_LIB=licensee_amd/lib/var/bias.so timeout -k 10 300 python -u -m pytest tests/test_gpu_corpus_sizes.py -x -q --timeout 300 -m gpu -k "130-post or 600-post" > gpurun_out/t_bias.log 2>&1; echo "bias variant rc=$?"; grep -E "passed|failed|Error" gpurun_out/t_bias.log | tail -3
+for v in base head; do
   unset LICENSEE_DICE_LIB
   [ $v != base ] && export LICENSEE_DICE_LIB=licensee_amd/lib/var/$v.so
   rm -rf gpurun_out/split_$v
@@ -10,5 +11,5 @@ for v in base noplanes kloop_only head; do
   echo "== $v"; python tools/rocpd_summary.py gpurun_out/split_$v/run_results.db --match dice_post
 done
 unset LICENSEE_DICE_LIB
-bash tools/gpu_ab.sh 3 "--config 5-T600 --steps 10" base lib:noplanes lib:head
-bash tools/gpu_ab.sh 3 "--config 3 --steps 10" DICE_POST_PRUNE=0 lib:noplanes,DICE_POST_PRUNE=0 lib:head,DICE_POST_PRUNE=0
+bash tools/gpu_ab.sh 3 "--config 5-T600 --steps 10" base lib:head
+bash tools/gpu_ab.sh 3 "--config 3 --steps 10" DICE_POST_PRUNE=0 lib:head,DICE_POST_PRUNE=0
