@@ -883,6 +883,9 @@ __device__ __forceinline__ bool lane_eval(const uint32_t* crow32, const uint2* t
 #define POST_TOPK_SECOND 1
 #endif
 
+#ifndef POST_SCORE_NODIV
+#define POST_SCORE_NODIV 0
+#endif
 #ifndef POST_MATRIX_STORE
 #define POST_MATRIX_STORE 3
 #endif
@@ -953,7 +956,11 @@ __device__ __forceinline__ void score_file_t(uint32_t* crow32, const uint2* tcs,
             if (kMatrix) {
 #if POST_MATRIX_STORE == 3
                 __builtin_nontemporal_store(ov, orow + t);
+#if POST_SCORE_NODIV   // timing split only (results wrong): the score store without its division
+                __builtin_nontemporal_store((double)ov * (double)den, srow + t);
+#else
                 __builtin_nontemporal_store(dice_score(ov, den), srow + t);
+#endif
 #else
                 const double sc = dice_score(ov, den);
                 // diagnostics (POST_MATRIX_STORE, A/B builds only): bit 0 / 1 store overlaps / scores

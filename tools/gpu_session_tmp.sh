@@ -1,15 +1,11 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py tests/test_gpu_prune.py tests/test_gpu_parity.py -x -q --timeout 300 -m gpu > gpurun_out/t_post.log 2>&1 || { echo tests failed; tail -30 gpurun_out/t_post.log; exit 3; }
-tail -2 gpurun_out/t_post.log
-LICENSEE_DICE_LIB=licensee_amd/lib/var/bias.so timeout -k 10 300 python -u -m pytest tests/test_gpu_corpus_sizes.py -x -q --timeout 300 -m gpu -k "130-post or 600-post" > gpurun_out/t_bias.log 2>&1; echo "bias variant rc=$?"; grep -E "passed|failed|Error" gpurun_out/t_bias.log | tail -3
-for v in base head; do
+for v in base nodiv noscorestore; do
   unset LICENSEE_DICE_LIB
   [ $v != base ] && export LICENSEE_DICE_LIB=licensee_amd/lib/var/$v.so
-  rm -rf gpurun_out/split_$v
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/split_$v -o run -- python bench.py --config 5-T600 --steps 10 --warmup 2 --extra-configs= --no-cpu-baseline --no-extras > gpurun_out/split_$v.json 2> gpurun_out/split_$v.err || { echo "$v failed"; exit 3; }
-  echo "== $v"; python tools/rocpd_summary.py gpurun_out/split_$v/run_results.db --match dice_post
+  for cfg in 5-T600; do
+    rm -rf gpurun_out/diag_${v}_$cfg
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/diag_${v}_$cfg -o run -- python bench.py --config $cfg --steps 10 --warmup 2 --extra-configs= --no-cpu-baseline --no-extras > gpurun_out/diag_${v}_$cfg.json 2> gpurun_out/diag_${v}_$cfg.err || { echo "$v $cfg failed"; exit 3; }
+    echo "== $v $cfg"; python tools/rocpd_summary.py gpurun_out/diag_${v}_$cfg/run_results.db --match narrow
+  done
 done
-unset LICENSEE_DICE_LIB
-bash tools/gpu_ab.sh 3 "--config 5-T600 --steps 10" base lib:head
-bash tools/gpu_ab.sh 3 "--config 3 --steps 10" DICE_POST_PRUNE=0 lib:head,DICE_POST_PRUNE=0
