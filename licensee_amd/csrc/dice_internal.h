@@ -83,6 +83,7 @@ struct dice_ctx {
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_ld = 0;
     bool post_fast = false;
     int32_t post_mfma = 4;     // dense prefix: 4 dice_post_dense_mfma FP4 (default), 1 its int8 form, 0 the VALU kernel (DICE_POST_MFMA)
+    int32_t post_u8 = 0;       // FP4 dense kernel: u8 partial rows for files with <= 255 prefix words (DICE_POST_U8=1, A/B; slower)
     int32_t post_mfma_mt = 3;  // 32-file M-tiles per MFMA tile (T <= 640; DICE_POST_MFMA_MT=2 for A/B)
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --

@@ -53,20 +53,22 @@ namespace dice {
 #ifndef POST_DIAG
 #define POST_DIAG 0
 #endif
-// Dense partials as [n][tp] u16 rows. POST_PARTIALS_U8=1 (A/B build): u8 rows ([n][tp] bytes) for
-// files whose every prefix overlap fits a byte, u16 rows and a per-file flag for the others (about
-// one config-3 file in seven: a prefix of 1024 words can hold 600 of one template's) -- half the
-// round trip's bytes, but measured slower (config 3 all pairs 4.76 vs 4.64 ms, 5-T600 6.27 vs
-// 6.16 ms, 2 interleaved reps, profiles/r4h_partials_ab.txt): the kernels are latency-bound and the
-// byte rows cost a vote pass over the stage and a flag read per tile.
-#ifndef POST_PARTIALS_U8
-#define POST_PARTIALS_U8 0
-#endif
+// Dense partials: [n][tp] u16 rows, or (u8 mode, DICE_POST_U8=1, A/B, the FP4 dense kernel) a u8
+// row ([n][s8] u32 words of four partials, rows padded to 16 bytes) for every file whose prefix
+// holds at most 255 words -- no prefix overlap can exceed its popcount -- and a u16 row for the
+// others (17% of config-3 files at 20 prefix words), with a per-file flag (1: u16). Parity green,
+// 42% fewer partial bytes, and slower: the dense kernel 0.546 vs 0.479 ms on 5-T600 (its stores
+// are bound by store instructions, and mixed rows need both a u16 and a u8 store per piece), the
+// narrow kernels within 1%; 5-T600 5.13 vs 5.01 ms, all pairs 3.49 vs 3.45 (3 interleaved reps,
+// profiles/r5_dense_ab.txt). (Round 4's byte rows decided per file from the values, a vote over
+// the VALU kernel's stage, and measured slower too.)
 struct Partials {
     uint16_t* p16;   // [n][tp] u16 rows (files flagged 1)
-    uint32_t* p8;    // [n][tp / 4] u32 words of four u8 partials (files flagged 0)
-    uint8_t* flag;   // [n] 1: the file's row is the u16 one
+    uint32_t* p8;    // [n][s8] u32 words of four u8 partials (files flagged 0)
+    uint8_t* flag;   // [n] 1: the file's row is the u16 one; nullptr: every row is u16
 };
+// u32 words per u8 row: tp bytes rounded up to 16
+__host__ __device__ __forceinline__ int32_t u8_row_words(int32_t tp) { return (tp + 15) / 16 * 4; }
 
 // A/B: the dense kernel's file prefixes staged through LDS by coalesced loads (1) or loaded per lane (0)
 #ifndef POST_DENSE_LDS_PREFIX
@@ -237,31 +239,16 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
     }
 }
 
-// The stage's [file][template] u16 rows of a 64-file tile out to the partials ([n][tp] u16, or
-// with POST_PARTIALS_U8 the u8 rows and flags), one file per wave at a time.
+// The stage's [file][template] u16 rows of a 64-file tile out to the [n][tp] u16 partials, one file
+// per wave at a time (the VALU dense kernel writes u16 rows only).
 __device__ __forceinline__ void stage_out(const uint32_t* stage32, int32_t cs, int32_t tp, int64_t f0, int64_t nn,
                                           int wave, int nwaves, int lane, const Partials& pt) {
     for (int fi = wave; fi < kPostFiles; fi += nwaves) {
         const int64_t file = f0 + fi;
         if (file >= nn) break;
         const uint32_t* src = stage32 + (fi * cs) / 2;
-        // a byte row when every partial of the file fits a byte (one wave-wide vote), else u16
-        bool wide = !POST_PARTIALS_U8;
-        if (POST_PARTIALS_U8) {
-            bool any = false;
-            for (int32_t j = lane; j < tp / 2; j += kWave) any |= (src[j] & 0xFF00FF00u) != 0;
-            wide = __ballot(any) != 0;
-            if (lane == 0) pt.flag[file] = wide ? 1 : 0;
-        }
-        if (!wide) {
-            uint32_t* dst = pt.p8 + file * (tp / 4);
-            // bytes 0 and 2 of each u16 pair: v_perm_b32 packs four partials into one word
-            for (int32_t j = lane; j < tp / 4; j += kWave)
-                dst[j] = __builtin_amdgcn_perm(src[2 * j + 1], src[2 * j], 0x06040200u);
-        } else {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(pt.p16 + file * tp);
-            for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
-        }
+        uint32_t* dst = reinterpret_cast<uint32_t*>(pt.p16 + file * tp);
+        for (int32_t j = lane; j < tp / 2; j += kWave) dst[j] = src[j];
     }
 }
 
@@ -473,9 +460,12 @@ __device__ __forceinline__ v8i widen_b(uint32_t v) {
 // BIASED: the accumulators started at 2^23 (dice_post_dense_mfma, FP4 planes form), so the low 16
 // bits of their f32 encodings are the counts -- no conversion.
 constexpr int kSlabCols = 64;   // u16 per slab row (one wave's two N-tiles)
-template <int MT, bool BIASED, class ACC>
-__device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_t* slab, uint16_t* __restrict__ part,
-                                                int64_t f0, int64_t nn, int32_t tb, int32_t te, int32_t tp, int lane) {
+template <int MT, bool BIASED, bool U8OK, class ACC>
+__device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_t* slab, const Partials& pt,
+                                                const uint32_t* fc, int64_t f0, int64_t nn, int32_t tb, int32_t te,
+                                                int32_t tp, int wave, int lane) {
+    uint16_t* __restrict__ part = pt.p16;
+    const bool u8 = U8OK && pt.flag != nullptr;   // uniform (the FP4 kernels only)
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
     const int32_t rf = lf & 31, hf = lf >> 5;
@@ -500,6 +490,9 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_
                 }
             }
             __builtin_amdgcn_wave_barrier();
+            // u8 mode: a file's row is u16 only when its prefix holds more than 255 words
+            // (fc: the tile's prefix popcounts, dice_post_dense_mfma)
+            const uint32_t* fcp = fc + 32 * m + 16 * sh;
             if (nt == 2) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
@@ -507,14 +500,32 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_
                     const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabCols + piece * 8);
                     const int64_t file = f0 + 32 * m + 16 * sh + row;
                     const int32_t t = tb + piece * 8;
-                    if (POST_DENSE_AB != 1 && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+                    const bool w = !u8 || fcp[row] > 255u;
+                    if (POST_DENSE_AB != 1 && w && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
                 }
             } else {
                 const int row = lf >> 2, piece = lf & 3;
                 const uint4 v = *reinterpret_cast<const uint4*>(slab + row * kSlabCols + piece * 8);
                 const int64_t file = f0 + 32 * m + 16 * sh + row;
                 const int32_t t = tb + piece * 8;
-                if (POST_DENSE_AB != 1 && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+                const bool w = !u8 || fcp[row] > 255u;
+                if (POST_DENSE_AB != 1 && w && t < tpf && file < nn) *reinterpret_cast<uint4*>(part + file * tpf + t) = v;
+            }
+            if (u8) {
+                // the byte rows: lane = (file row lf >> 2, 16 templates lf & 3), 16 u16 from the slab
+                // packed to 16 bytes (bytes 0 and 2 of each u16 pair); rows padded to 16 bytes, so a
+                // piece that starts below tp may run into the padding
+                const int row = lf >> 2, p16 = lf & 3;
+                const uint4 a = *reinterpret_cast<const uint4*>(slab + row * kSlabCols + 16 * p16);
+                const uint4 c = *reinterpret_cast<const uint4*>(slab + row * kSlabCols + 16 * p16 + 8);
+                const uint4 v = make_uint4(__builtin_amdgcn_perm(a.y, a.x, 0x06040200u), __builtin_amdgcn_perm(a.w, a.z, 0x06040200u),
+                                           __builtin_amdgcn_perm(c.y, c.x, 0x06040200u), __builtin_amdgcn_perm(c.w, c.z, 0x06040200u));
+                const int64_t file = f0 + 32 * m + 16 * sh + row;
+                const int32_t t = tb + 16 * p16;
+                if (POST_DENSE_AB != 1 && fcp[row] <= 255u && t < te && t < tpf && file < nn)
+                    *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(pt.p8 + file * u8_row_words(tpf)) + t) = v;
+                if (wave == 0 && lf < 16 && f0 + 32 * m + 16 * sh + lf < nn)
+                    pt.flag[f0 + 32 * m + 16 * sh + lf] = fcp[lf] > 255u ? 1 : 0;
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -524,7 +535,7 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_
 template <int DP, int NTW, int NW, int MT, bool F4 = false>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
-    const uint64_t* __restrict__ dmask, uint16_t* __restrict__ part, const int32_t* __restrict__ idx,
+    const uint64_t* __restrict__ dmask, const Partials pt, const int32_t* __restrict__ idx,
     const uint32_t* __restrict__ pn) {
     // MT 32-file M-tiles per tile; the prefix buffer is doubled when LDS allows (one barrier per
     // tile; every shipped shape since the 16 x 64 slabs), else one buffer and a second barrier
@@ -536,12 +547,17 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     constexpr int kPreWords = kTF * DP;
     constexpr int kPer = (kPreWords + NW * kWave - 1) / (NW * kWave);   // prefix words per thread
     constexpr int kCols = NTW == 2 && NW == 12 ? 640 : NW * NTW * 32;   // the workgroup's template columns
-    constexpr size_t kFixed = (size_t)DP * kCols * 8 + (size_t)NW * 16 * kSlabCols * 2;
+    constexpr size_t kFixed = (size_t)DP * kCols * 8 + (size_t)NW * 16 * kSlabCols * 2 + 3 * (size_t)kTF * 4;
     constexpr int kBufs = kFixed + 2 * (size_t)kTF * kPreStride * 8 <= 160 * 1024 ? 2 : 1;
     __shared__ uint64_t pre[kBufs][kTF * kPreStride];
     __shared__ uint64_t bm[DP * kCols];              // template masks, word-major (<= 110 KiB at DP 20)
     __shared__ uint16_t tslab[NW][16 * kSlabCols];   // per-wave 16 x 64 transpose slab (2 KiB)
-    static_assert(sizeof(pre) + sizeof(bm) + sizeof(tslab) <= 160 * 1024, "one workgroup's LDS");
+    // u8 mode: the prefix popcount of each file of a tile, a ring of three: tile i reads slot i % 3,
+    // its store_pre adds the next tile's into slot (i + 1) % 3, and it zeroes slot (i + 2) % 3 -- each
+    // step a barrier away from the last use of its slot
+    __shared__ uint32_t fcnt[3][kTF];
+    static_assert(sizeof(pre) + sizeof(bm) + sizeof(tslab) + sizeof(fcnt) <= 160 * 1024, "one workgroup's LDS");
+    const bool u8 = F4 && pt.flag != nullptr;   // uniform (byte rows: the FP4 kernels)
     constexpr bool kBiased = F4 && POST_DENSE_PLANES && POST_DENSE_BIAS;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
@@ -565,11 +581,12 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             pv[k] = (i < kPreWords && file < nn && d < D) ? rows[(idx ? (int64_t)idx[file] : file) * w64 + d] : 0;
         }
     };
-    auto store_pre = [&](int buf, const uint64_t (&pv)[kPer]) {
+    auto store_pre = [&](int buf, const uint64_t (&pv)[kPer], int slot) {
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const int i = (int)threadIdx.x + k * NW * kWave;
             if (i < kPreWords) {
+                if (u8 && pv[k]) atomicAdd(&fcnt[slot][i / DP], (uint32_t)__builtin_popcountll(pv[k]));
                 const int at = (i / DP) * kPreStride + i % DP;
                 if constexpr (F4 && POST_DENSE_PLANES) {   // low and high dwords in two planes
                     uint32_t* p32 = reinterpret_cast<uint32_t*>(pre[buf]);
@@ -592,17 +609,25 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
             bm[i] = v;
         }
     }
+    if (u8 && threadIdx.x < kTF) {
+        fcnt[0][threadIdx.x] = 0;
+        fcnt[1][threadIdx.x] = 0;
+    }
+    if (u8) __syncthreads();
     uint64_t pv[kPer];
     load_pre(f0, pv);
-    store_pre(0, pv);
+    store_pre(0, pv, 0);
     __syncthreads();
+    int slot = 0;   // fcnt slot of the current tile (uniform)
     v16f bias;   // 2^23: the accumulators' f32 encodings then hold the counts in their low bits
 #pragma unroll
     for (int g = 0; g < 16; ++g) bias[g] = 8388608.0f;
-    for (int buf = 0; f0 < nn; f0 += stride, buf = (buf + 1) % kBufs) {
+    for (int buf = 0; f0 < nn; f0 += stride, buf = (buf + 1) % kBufs, slot = slot == 2 ? 0 : slot + 1) {
         // unconditional (zeros past the end): a load under `if (more)` left pending on the skip path
         // would make the loop head wait vmcnt(0) for this tile's stores
         load_pre(f0 + stride, pv);
+        const int nslot = slot == 2 ? 0 : slot + 1, zslot = nslot == 2 ? 0 : nslot + 1;
+        if (u8 && threadIdx.x < kTF) fcnt[zslot][threadIdx.x] = 0;
         using Acc = typename std::conditional<F4, v16f, v16i>::type;
         Acc acc[MT][NTW];
         if constexpr (!kBiased) {
@@ -687,8 +712,9 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
         // the next tile's prefixes into LDS before this tile's stores are issued: the wait on their
         // loads (vmcnt counts stores too, in order) then finds only the previous tile's stores,
         // issued a whole k-loop ago, and this tile's stores drain under the next tile's MFMAs
-        store_pre((buf + 1) % kBufs, pv);
-        if (POST_DENSE_AB != 3) mfma_store_tile<MT, kBiased>(acc, tslab[wave], part, f0, nn, tb, tb + 32 * nw_tiles, tp, lane);
+        store_pre((buf + 1) % kBufs, pv, nslot);
+        if (POST_DENSE_AB != 3)
+            mfma_store_tile<MT, kBiased, F4>(acc, tslab[wave], pt, fcnt[slot], f0, nn, tb, tb + 32 * nw_tiles, tp, wave, lane);
         __syncthreads();   // the next tile's prefixes are complete (MT = 2: the other buffer)
     }
 }
@@ -719,7 +745,7 @@ __device__ __forceinline__ void copy_in(uint32_t* crow32, const uint32_t (&part)
 template <int PJ, bool CLAMP>
 __device__ __forceinline__ void load_partials(const Partials& pt, int64_t pos, int32_t tp, bool wide, int lane,
                                               uint32_t (&part)[PJ]) {
-    const uint32_t* src = wide ? reinterpret_cast<const uint32_t*>(pt.p16 + pos * tp) : pt.p8 + pos * (tp / 4);
+    const uint32_t* src = wide ? reinterpret_cast<const uint32_t*>(pt.p16 + pos * tp) : pt.p8 + pos * u8_row_words(tp);
     const int32_t nw = wide ? tp / 2 : tp / 4;
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
@@ -1057,7 +1083,7 @@ constexpr int pairs_per_lane() { return (TPMAX / 2 + kWave - 1) / kWave; }   // 
 // >= D and walked (walk_short / walk_long) after the file's dense partials (from
 // dice_post_dense) are copied in (every entry: no zeroing between files); scoring reads the counters and reduces over the
 // wave. The LDS footprint (~74 KiB) and <= 64 VGPRs leave room for two workgroups per CU.
-template <bool kMatrix, int KM, int TPMAX>
+template <bool kMatrix, int KM, int TPMAX, bool U8>
 __device__ __forceinline__ void post_narrow_body(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -1115,7 +1141,7 @@ __device__ __forceinline__ void post_narrow_body(
         if ((lw & (kNarrowWaves - 1)) == (uint32_t)wave) tsc[wave][lw / kNarrowWaves] = make_uint2(twf, tlen);
     }
     // the tile's partial formats (bit l: position f0 + l has a u16 row)
-    const uint64_t tov = POST_PARTIALS_U8 ? __ballot(pt.flag[f0 + min(lane, nt - 1)] != 0) : ~0ull;
+    const uint64_t tov = U8 ? __ballot(pt.flag[f0 + min(lane, nt - 1)] != 0) : ~0ull;
     // match mode: the next file's dense partials, prefetched while the wave scores the previous
     // file (the matrix kernel loads them at the file's start: file_postings LATE); matrix mode with
     // POST_MATRIX_PREFETCH: the next file's partials and first word chunks, loaded before this
@@ -1124,7 +1150,10 @@ __device__ __forceinline__ void post_narrow_body(
     constexpr int kNC = kMatrix ? POST_CHUNKS_MATRIX : POST_CHUNKS_MATCH;
     uint32_t pre[kPJ];
     uint64_t xs0[kPF ? kNC : 1];
-    if ((!kMatrix || kPF) && wave < nt) load_partials<kPJ, false>(pt, f0 + wave, tp, (tov >> wave) & 1, lane, pre);
+    // (U8 match mode loads them at the file's start, as the matrix kernel does: the prefetch's
+    // registers beside the byte-row logic exceed 64 VGPRs)
+    constexpr bool kEarly = (!kMatrix && !U8) || kPF;
+    if (kEarly && wave < nt) load_partials<kPJ, U8>(pt, f0 + wave, tp, (tov >> wave) & 1, lane, pre);
     if (kPF && wave < nt && pb0 < w64) load_chunks<kNC>(rows + (f0 + wave) * w64, w64, pb0, lane, *reinterpret_cast<uint64_t (*)[kNC]>(xs0));
     for (int fi = wave; fi < kPostFiles; fi += kNarrowWaves) {
         const int64_t pos = f0 + fi;
@@ -1136,11 +1165,11 @@ __device__ __forceinline__ void post_narrow_body(
         // they stayed live as ~30 SGPRs and several VGPRs and spilled (the matrix kernel to scratch)
         int32_t Tf = T, tpf = tp, ldf = ld;
         int lanef = lane;   // likewise every lane-derived constant (lane + 64 j, lane addresses)
-        if (kMatrix) asm volatile("" : "+s"(Tf), "+s"(tpf), "+s"(ldf), "+v"(lanef));
+        if (kMatrix || U8) asm volatile("" : "+s"(Tf), "+s"(tpf), "+s"(ldf), "+v"(lanef));
         // this file's dense partials start its counter row (matrix mode without prefetch: inside
         // file_postings)
         const bool wide = (tov >> fi) & 1;
-        if (!kMatrix || kPF) copy_in<kPJ>(crow32, pre, tpf, wide, lanef);
+        if (kEarly) copy_in<kPJ>(crow32, pre, tpf, wide, lanef);
         uint32_t wf;
         int32_t lf;
         if (kMatrix) {
@@ -1157,12 +1186,12 @@ __device__ __forceinline__ void post_narrow_body(
                                                        plong, crow32, lanef,
                                                        reinterpret_cast<const uint64_t (*)[kNC]>(xs0));
         } else {
-            file_postings<kWCap, kMatrix, kPJ>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow, plong,
+            file_postings<kWCap, !kEarly, kPJ, kNC>(row, w64, pb0, pt, pos, wide, tpf, wq[wave], lq[wave], prow, plong,
                                                crow32, lanef);
         }
         // the wave's next file's partials (and with kPF its first chunks) fly while this one is scored
-        if ((!kMatrix || kPF) && fi + kNarrowWaves < nt)
-            load_partials<kPJ, false>(pt, pos + kNarrowWaves, tpf, (tov >> (fi + kNarrowWaves)) & 1, lane, pre);
+        if (kEarly && fi + kNarrowWaves < nt)
+            load_partials<kPJ, U8>(pt, pos + kNarrowWaves, tpf, (tov >> (fi + kNarrowWaves)) & 1, lane, pre);
         if (kPF && fi + kNarrowWaves < nt && pb0 < w64)
             load_chunks<kNC>(rows + (pos + kNarrowWaves) * w64, w64, pb0, lane, *reinterpret_cast<uint64_t (*)[kNC]>(xs0));
 
@@ -1175,7 +1204,9 @@ __device__ __forceinline__ void post_narrow_body(
 
 // Match mode held to 64 VGPRs (8 waves per SIMD: two workgroups per CU); the matrix mode's
 // top-k slots need more registers and run at the occupancy they get.
-template <int TPMAX>
+// U8: the partials come as byte rows where the prefix allows (Partials.flag); the u16-only form is a
+// separate instantiation, so its registers are those of the rounds before byte rows
+template <int TPMAX, bool U8>
 __global__ __launch_bounds__(narrow_waves<false>() * kWave) __attribute__((amdgpu_waves_per_eu(POST_NARROW_OCC, POST_NARROW_OCC))) void dice_post_narrow_match(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -1184,7 +1215,7 @@ __global__ __launch_bounds__(narrow_waves<false>() * kWave) __attribute__((amdgp
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
-    post_narrow_body<false, 1, TPMAX>(rows, n, w64, D, T, tp, pt, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+    post_narrow_body<false, 1, TPMAX, U8>(rows, n, w64, D, T, tp, pt, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
@@ -1194,7 +1225,7 @@ __global__ __launch_bounds__(narrow_waves<false>() * kWave) __attribute__((amdgp
 #ifndef POST_MATRIX_OCC
 #define POST_MATRIX_OCC 6
 #endif
-template <int KM, int TPMAX>
+template <int KM, int TPMAX, bool U8>
 __global__ __launch_bounds__(narrow_waves<true>() * kWave) __attribute__((amdgpu_waves_per_eu(POST_MATRIX_OCC, POST_MATRIX_OCC))) void dice_post_narrow_matrix(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t T, int32_t tp,
     const Partials pt, const uint16_t* __restrict__ prow, const uint16_t* __restrict__ plong,
@@ -1203,7 +1234,7 @@ __global__ __launch_bounds__(narrow_waves<true>() * kWave) __attribute__((amdgpu
     double* __restrict__ score_out, int32_t k, uint32_t* __restrict__ mov, double* __restrict__ msc,
     int32_t* __restrict__ tki, double* __restrict__ tks, bool corpus_fast,
     const int32_t* __restrict__ idx, const uint32_t* __restrict__ pn, int32_t ld) {
-    post_narrow_body<true, KM, TPMAX>(rows, n, w64, D, T, tp, pt, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
+    post_narrow_body<true, KM, TPMAX, U8>(rows, n, w64, D, T, tp, pt, prow, plong, tc, wfp, lenp, ccp, thr, best_out, ov_out,
                                score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
@@ -1331,6 +1362,8 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     // the dense prefix on the matrix cores (dice_post_dense_mfma) unless DICE_POST_MFMA=0
     const char* mt = getenv("DICE_POST_MFMA_MT");   // 32-file M-tiles per MFMA tile (2 or 3; A/B)
     c->post_mfma_mt = (mt && *mt == '2') ? 2 : 3;
+    const char* u8 = getenv("DICE_POST_U8");   // byte partial rows where the prefix allows (A/B: 1; slower)
+    c->post_u8 = u8 && *u8 == '1';
     // corpus part of the 24-bit compare envelope: |Lf| < 2^11 (overlaps), 1 <= base < 2^18,
     // template lengths < 2^20 and 200 |Lf| < 1024 base (every fast-file score < 1024)
     c->post_fast = true;
@@ -1351,22 +1384,24 @@ int post_setup(dice_ctx* c, const dice_templates* t) {
     return DICE_OK;
 }
 
-// The batch's partials region: [capacity][tp] u16 rows (| [capacity][tp] u8 rows | [capacity] flags
-// in a POST_PARTIALS_U8 build).
-static Partials partials_of(const dice_ctx* c, const dice_batch* b) {
+// The batch's partials region: [capacity][tp] u16 rows | [capacity][s8] u32 words of u8 rows |
+// [capacity] flags. u8: the launch writes byte rows where a file's prefix allows (the matrix-core
+// dense kernels, DICE_POST_U8); otherwise flag = nullptr and every row is u16.
+static int32_t partials_s8(const dice_ctx* c) { return u8_row_words(c->post_tp); }
+static Partials partials_of(const dice_ctx* c, const dice_batch* b, bool u8) {
     char* base = reinterpret_cast<char*>(b->d_pdense);
-    const size_t n16 = (size_t)b->capacity * c->post_tp * 2, n8 = (size_t)b->capacity * c->post_tp;
+    const size_t n16 = (size_t)b->capacity * c->post_tp * 2, n8 = (size_t)b->capacity * partials_s8(c) * 4;
     Partials pt;
     pt.p16 = reinterpret_cast<uint16_t*>(base);
     pt.p8 = reinterpret_cast<uint32_t*>(base + n16);
-    pt.flag = reinterpret_cast<uint8_t*>(base + n16 + n8);
+    pt.flag = u8 ? reinterpret_cast<uint8_t*>(base + n16 + n8) : nullptr;
     return pt;
 }
 
 template <int DP>
 static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t groups, const int32_t* idx,
-                         const uint32_t* pn) {
-    if (c->post_mfma && !POST_PARTIALS_U8) {
+                         const uint32_t* pn, const Partials& pt) {
+    if (c->post_mfma) {
         // kMfmaNT N-tiles of 32 templates per wave: 10 waves cover 640 templates (tp <= 640), 11 704;
         // persistent workgroups (one per CU: 10-11 waves at 3 per SIMD), the next tile's prefixes
         // loaded during this one
@@ -1382,21 +1417,21 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
         const int64_t g = std::min<int64_t>(std::min<int64_t>(groups, mtiles), (int64_t)c->n_cu);
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3((small ? 12 : 11) * kWave), 0, s,
                            (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->post_tp,
-                           (const uint64_t*)c->d_pdmt, partials_of(c, b).p16, idx, pn);
+                           (const uint64_t*)c->d_pdmt, pt, idx, pn);
         return;
     }
     if constexpr (DP <= kPostMaxDense) {   // (the VALU kernel's prefix is capped at 16 words: post_setup)
         auto kern = c->post_tp <= 608 ? dice_post_dense<DP, 608> : dice_post_dense<DP, kPostMaxTpad>;
         hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kPostWaves * kWave), 0, s,
                            (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
-                           (const uint64_t*)c->d_pdm, partials_of(c, b), idx, pn);
+                           (const uint64_t*)c->d_pdm, pt, idx, pn);
     }
 }
 
 int post_reserve(dice_ctx* c, dice_batch* b) {
-    // u16 rows, and with POST_PARTIALS_U8 the u8 rows and flags (partials_of)
-    const size_t need = (size_t)b->capacity * c->post_tp * 2 +
-                        (POST_PARTIALS_U8 ? (size_t)b->capacity * c->post_tp + (size_t)b->capacity : 0);
+    // u16 rows, u8 rows and flags (partials_of)
+    const size_t need = (size_t)b->capacity * c->post_tp * 2 + (size_t)b->capacity * partials_s8(c) * 4 +
+                        (size_t)b->capacity;
     if (b->pdense_bytes < need) {
         if (b->d_pdense) (void)hipFree(b->d_pdense);
         b->d_pdense = nullptr;
@@ -1420,26 +1455,28 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     // (the narrow kernel's workgroups resident per CU: two 16-wave, three 8-wave)
     constexpr int kNarrowWaves = narrow_waves<kMatrix>();
     const int64_t groups = idx ? std::min<int64_t>(tiles, (kNarrowWaves == 16 ? 2 : 3) * (int64_t)c->n_cu) : tiles;
-    const Partials pt = partials_of(c, b);
-    if (c->post_dense == 0 || (POST_DIAG & 1)) {
-        // no dense prefix: zero partials (u8 rows with flags 0; u16 rows when every row is u16)
+    const bool dense = c->post_dense > 0 && !(POST_DIAG & 1);
+    const Partials pt = partials_of(c, b, dense && c->post_mfma == 4 && c->post_u8);
+    if (!dense) {
+        // no dense prefix: zero u16 partials
         const size_t rows = (size_t)(idx ? b->capacity : b->n);
-        const hipError_t e = POST_PARTIALS_U8
-                                 ? (hipMemsetAsync(pt.p8, 0, rows * c->post_tp, s) == hipSuccess
-                                        ? hipMemsetAsync(pt.flag, 0, rows, s) : hipErrorUnknown)
-                                 : hipMemsetAsync(pt.p16, 0, rows * c->post_tp * 2, s);
-        if (e != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
+        if (hipMemsetAsync(pt.p16, 0, rows * c->post_tp * 2, s) != hipSuccess)
+            return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
     } else {
         switch ((c->post_dense + 3) / 4) {
-            case 1: launch_dense<4>(c, b, s, groups, idx, pn); break;
-            case 2: launch_dense<8>(c, b, s, groups, idx, pn); break;
-            case 3: launch_dense<12>(c, b, s, groups, idx, pn); break;
-            case 4: launch_dense<16>(c, b, s, groups, idx, pn); break;
-            default: launch_dense<20>(c, b, s, groups, idx, pn); break;
+            case 1: launch_dense<4>(c, b, s, groups, idx, pn, pt); break;
+            case 2: launch_dense<8>(c, b, s, groups, idx, pn, pt); break;
+            case 3: launch_dense<12>(c, b, s, groups, idx, pn, pt); break;
+            case 4: launch_dense<16>(c, b, s, groups, idx, pn, pt); break;
+            default: launch_dense<20>(c, b, s, groups, idx, pn, pt); break;
         }
     }
-    auto kern = c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608> : dice_post_narrow_match<608>)
-                                  : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad> : dice_post_narrow_match<kPostMaxTpad>);
+    auto kern = pt.flag ? (c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608, true> : dice_post_narrow_match<608, true>)
+                                             : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad, true>
+                                                        : dice_post_narrow_match<kPostMaxTpad, true>))
+                        : (c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<KM, 608, false> : dice_post_narrow_match<608, false>)
+                                             : (kMatrix ? dice_post_narrow_matrix<KM, kPostMaxTpad, false>
+                                                        : dice_post_narrow_match<kPostMaxTpad, false>));
     hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kNarrowWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        pt, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,

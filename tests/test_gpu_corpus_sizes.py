@@ -50,8 +50,10 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
 
 # the postings kernels' dense-prefix variants: the matrix-core kernel (default, int8
 # and FP4 forms) with 3 or 2 32-file M-tiles per tile (12 waves, tp <= 640) and its 11-wave form
-# above 640 templates (672, 700), and the VALU kernel (DICE_POST_MFMA=0)
+# above 640 templates (672, 700), the VALU kernel (DICE_POST_MFMA=0), and the FP4 kernel with byte
+# partial rows for files with <= 255 prefix words (DICE_POST_U8=1, A/B)
 PREFIX_VARIANTS = {'fp4-mt3': {}, 'fp4-mt2': {'DICE_POST_MFMA_MT': '2'}, 'valu': {'DICE_POST_MFMA': '0'},
+                   'fp4-u8': {'DICE_POST_U8': '1'},
                    'int8-mt3': {'DICE_POST_MFMA': '1'}, 'int8-mt2': {'DICE_POST_MFMA': '1', 'DICE_POST_MFMA_MT': '2'}}
 
 

@@ -28,9 +28,10 @@ def _resources(src):
 def test_postings_kernels_fit_8_waves_without_scratch():
     res = _resources('dice_post.hip')
     # (the matrix kernels run 8-wave workgroups at 6 waves per SIMD: three per CU)
-    for name, occ in (('dice_post_narrow_match<608>', 8), ('dice_post_narrow_matrix<1, 608>', 6),
-                      ('dice_post_dense<16, 608>', 8), ('dice_post_narrow_match<704>', 8),
-                      ('dice_post_narrow_matrix<1, 704>', 6)):
+    # (each narrow kernel in its u16-partials and byte-row (U8) forms)
+    names = [(f'dice_post_narrow_match<{tp}, {u8}>', 8) for tp in (608, 704) for u8 in ('false', 'true')]
+    names += [(f'dice_post_narrow_matrix<1, {tp}, {u8}>', 6) for tp in (608, 704) for u8 in ('false', 'true')]
+    for name, occ in names + [('dice_post_dense<16, 608>', 8)]:
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0', (name, r)
         assert r['VGPRs Spill'] == '0', (name, r)
