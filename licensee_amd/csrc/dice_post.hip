@@ -465,7 +465,7 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_
                                                 const uint32_t* fc, int64_t f0, int64_t nn, int32_t tb, int32_t te,
                                                 int32_t tp, int wave, int lane) {
     uint16_t* __restrict__ part = pt.p16;
-    const bool u8 = U8OK && pt.flag != nullptr;   // uniform (the FP4 kernels only)
+    constexpr bool u8 = U8OK;
     int32_t tpf = tp, lf = lane;
     asm volatile("" : "+s"(tpf), "+v"(lf));   // addresses formed here, per tile
     const int32_t rf = lf & 31, hf = lf >> 5;
@@ -532,7 +532,7 @@ __device__ __forceinline__ void mfma_store_tile(const ACC (&acc)[MT][2], uint16_
     }
 }
 
-template <int DP, int NTW, int NW, int MT, bool F4 = false>
+template <int DP, int NTW, int NW, int MT, bool F4 = false, bool U8 = false>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3))) void dice_post_dense_mfma(
     const uint64_t* __restrict__ rows, int64_t n, int32_t w64, int32_t D, int32_t tp,
     const uint64_t* __restrict__ dmask, const Partials pt, const int32_t* __restrict__ idx,
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
     // step a barrier away from the last use of its slot
     __shared__ uint32_t fcnt[3][kTF];
     static_assert(sizeof(pre) + sizeof(bm) + sizeof(tslab) + sizeof(fcnt) <= 160 * 1024, "one workgroup's LDS");
-    const bool u8 = F4 && pt.flag != nullptr;   // uniform (byte rows: the FP4 kernels)
+    constexpr bool u8 = F4 && U8;   // byte rows (DICE_POST_U8=1): a separate instantiation
     constexpr bool kBiased = F4 && POST_DENSE_PLANES && POST_DENSE_BIAS;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (int)rfl(threadIdx.x >> 6);
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(3, 3
         // issued a whole k-loop ago, and this tile's stores drain under the next tile's MFMAs
         store_pre((buf + 1) % kBufs, pv, nslot);
         if (POST_DENSE_AB != 3)
-            mfma_store_tile<MT, kBiased, F4>(acc, tslab[wave], pt, fcnt[slot], f0, nn, tb, tb + 32 * nw_tiles, tp, wave, lane);
+            mfma_store_tile<MT, kBiased, u8>(acc, tslab[wave], pt, fcnt[slot], f0, nn, tb, tb + 32 * nw_tiles, tp, wave, lane);
         __syncthreads();   // the next tile's prefixes are complete (MT = 2: the other buffer)
     }
 }
@@ -1407,7 +1407,8 @@ static void launch_dense(dice_ctx* c, dice_batch* b, hipStream_t s, int64_t grou
         // loaded during this one
         const bool small = c->post_tp <= 640;
         auto kern = c->post_mfma == 4
-                        ? (small ? (c->post_mfma_mt == 3 ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3, true>
+                        ? (small ? (c->post_mfma_mt == 3 ? (pt.flag ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3, true, true>
+                                                                    : dice_post_dense_mfma<DP, kMfmaNT, 12, 3, true>)
                                                          : dice_post_dense_mfma<DP, kMfmaNT, 12, 2, true>)
                                  : dice_post_dense_mfma<DP, kMfmaNT, 11, 2, true>)
                         : (small ? (c->post_mfma_mt == 3 ? dice_post_dense_mfma<DP, kMfmaNT, 12, 3>
@@ -1456,7 +1457,9 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     constexpr int kNarrowWaves = narrow_waves<kMatrix>();
     const int64_t groups = idx ? std::min<int64_t>(tiles, (kNarrowWaves == 16 ? 2 : 3) * (int64_t)c->n_cu) : tiles;
     const bool dense = c->post_dense > 0 && !(POST_DIAG & 1);
-    const Partials pt = partials_of(c, b, dense && c->post_mfma == 4 && c->post_u8);
+    // (byte rows: the FP4 kernel at 3 M-tiles, tp <= 640, the one instantiated with them)
+    const Partials pt = partials_of(c, b, dense && c->post_mfma == 4 && c->post_u8 && c->post_tp <= 640 &&
+                                              c->post_mfma_mt == 3);
     if (!dense) {
         // no dense prefix: zero u16 partials
         const size_t rows = (size_t)(idx ? b->capacity : b->n);

@@ -49,8 +49,9 @@ def test_config3_pruned_kernel_fits_8_waves_without_scratch():
 def test_mfma_dense_prefix_kernel_fits_2_waves_without_scratch():
     res = _resources('dice_post.hip')
     # int8 (false) and FP4 (true) forms; the FP4 kernel at the 20-word prefix the config-3 corpus uses
-    names = [f'dice_post_dense_mfma<{dp}, 2, {nw}, {mt}, {f4}>' for dp, f4 in ((16, 'false'), (16, 'true'), (20, 'true'))
+    names = [f'dice_post_dense_mfma<{dp}, 2, {nw}, {mt}, {f4}, false>' for dp, f4 in ((16, 'false'), (16, 'true'), (20, 'true'))
              for nw, mt in ((12, 2), (12, 3), (11, 2))]
+    names.append('dice_post_dense_mfma<20, 2, 12, 3, true, true>')   # byte partial rows (DICE_POST_U8=1)
     for name in names:
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0' and r['VGPRs Spill'] == '0', (name, r)
