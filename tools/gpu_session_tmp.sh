@@ -1,8 +1,8 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py tests/test_gpu_prune.py tests/test_gpu_parity.py -x -q --timeout 300 -m gpu > gpurun_out/t_u8b.log 2>&1 || { echo tests failed; tail -30 gpurun_out/t_u8b.log; exit 3; }
-tail -2 gpurun_out/t_u8b.log
-for v in base head; do
+timeout -k 10 900 python -u -m pytest tests/test_gpu_corpus_sizes.py tests/test_gpu_slowpath.py tests/test_gpu_parity.py tests/test_gpu_golden.py tests/test_gpu_api.py tests/test_gpu_sharded.py -x -q --timeout 300 -m gpu > gpurun_out/t_vec4.log 2>&1 || { echo tests failed; tail -30 gpurun_out/t_vec4.log; exit 3; }
+tail -2 gpurun_out/t_vec4.log
+for v in base novec4; do
   unset LICENSEE_DICE_LIB
   [ $v != base ] && export LICENSEE_DICE_LIB=licensee_amd/lib/var/$v.so
   rm -rf gpurun_out/split_$v
@@ -10,4 +10,4 @@ for v in base head; do
   echo "== $v"; python tools/rocpd_summary.py gpurun_out/split_$v/run_results.db --match dice_post
 done
 unset LICENSEE_DICE_LIB
-bash tools/gpu_ab.sh 3 "--config 5-T600 --steps 10" base lib:head
+bash tools/gpu_ab.sh 3 "--config 5-T600 --steps 10" base lib:novec4
