@@ -91,7 +91,9 @@ def test_config3_files(config3, monkeypatch):
 KNOBS = [{}, {'DICE_PRUNE_MAX_EVALS': '1'}, {'DICE_PRUNE_MAX_EVALS': '0'}, {'DICE_PRUNE_ROUTE': '0'},
          {'DICE_PRUNE_ROUTE_AT': '1'}, {'DICE_PRUNE_ROUTE': '600', 'DICE_PRUNE_ROUTE_AT': '4'},
          {'DICE_PRUNE_SURVIVORS': '32'}, {'DICE_PRUNE_MAX_EVALS': '1', 'DICE_PRUNE_SURVIVORS': '1'},
-         {'DICE_PRUNE_ROUTE': '0', 'DICE_PRUNE_SURVIVORS': '3'}]
+         {'DICE_PRUNE_ROUTE': '0', 'DICE_PRUNE_SURVIVORS': '3'},
+         # the deferred files' partials as byte rows where their prefix allows (indexed positions)
+         {'DICE_PRUNE_ROUTE': '0', 'DICE_POST_U8': '1'}]
 
 
 @pytest.mark.parametrize('knob', range(len(KNOBS)))
