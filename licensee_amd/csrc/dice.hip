@@ -539,7 +539,12 @@ static int upload_tail(dice_batch* b, int64_t n, const uint32_t* wf, const int32
         HIP_TRY(hipMemsetAsync(b->d_len + n, 0, (size_t)(npad - n) * 4, s));
         HIP_TRY(hipMemsetAsync(b->d_cc + n, 0, (size_t)(npad - n), s));
     }
-    if (c->kind == 3) return DICE_OK;   // the postings kernel reads the row-major bitsets
+    if (c->kind == 3) {   // the postings kernel reads the row-major bitsets
+        b->n_long = 0;
+        if (c->prune)
+            for (int64_t i = 0; i < n; ++i) b->n_long += wf[i] > c->prune_max_lf;
+        return DICE_OK;
+    }
     const int64_t total = n_tiles * c->wq * kWave;
     const unsigned grid = (unsigned)((total + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(dice_pack_tiles, dim3(grid), dim3(kBlock), 0, s, b->d_rows, n, c->w64, c->wq,
@@ -653,10 +658,13 @@ static int batch_match(dice_batch* b, double thr, void* stream, bool confidence)
         if (rc != DICE_OK) return rc;
     } else if (c->kind == 3) {
         // the T > 64 kernels write Dice#confidence outputs themselves
-        int rc = c->prune ? dice::prune_launch_match(c, b, thr, s, confidence)
-                          : dice::post_launch_match(c, b, thr, s, confidence);
+        // (dice_match on a batch of mostly long files: the postings kernels, see prune_setup)
+        const bool prune = c->prune && (confidence || c->prune_long_route == 0 || b->n_long < 0 ||
+                                        b->n_long * c->prune_long_route < b->n);
+        int rc = prune ? dice::prune_launch_match(c, b, thr, s, confidence)
+                       : dice::post_launch_match(c, b, thr, s, confidence);
         if (rc != DICE_OK) return rc;
-        b->last_match = c->prune ? 2 : 1;
+        b->last_match = prune ? 2 : 1;
     } else {
         hipLaunchKernelGGL(dice_dense_match<kTT>, dim3(grid), dim3(kBlock), 0, s, b->d_tiles, b->n, c->wq,
                            c->d_tq, c->d_tc, c->T, c->tpad, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
@@ -960,7 +968,12 @@ int small_upload(dice_ctx* c, dice_batch* b, const dice_files* f, const SmallLay
     std::memcpy(h + L.rows, f->bits, (size_t)n * c->w64 * 8);
     b->n = n;
     HIP_TRY(hipMemcpyAsync(b->d_in, h, L.rows + (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, c->stream));
-    if (c->kind == 3) return DICE_OK;
+    if (c->kind == 3) {   // (dice_match's long-file routing, upload_tail)
+        b->n_long = 0;
+        if (c->prune)
+            for (int64_t i = 0; i < n; ++i) b->n_long += f->wordset_size[i] > c->prune_max_lf;
+        return DICE_OK;
+    }
     const int64_t n_tiles = npad / kWave;
     const int64_t total = n_tiles * c->wq * kWave;
     hipLaunchKernelGGL(dice_pack_tiles, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,

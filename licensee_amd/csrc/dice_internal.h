@@ -89,6 +89,8 @@ struct dice_ctx {
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --
     // group bytes, constants, CC masks, template index | record offset, records, slot bounds
     bool prune = false, prune_zero_base = false;
+    uint32_t prune_max_lf = 0;       // largest template |Lf| (the long-file test of dice_match's routing)
+    int32_t prune_long_route = 4;    // dice_match: postings kernels when >= 1/N of a batch's files are long (0: never)
     uint32_t prune_wf_noclamp = 0;   // |W_F| from which the bound's length term needs no clamp
     void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
          *d_p4slot = nullptr, *d_p4q32 = nullptr, *d_p4s32 = nullptr;
@@ -179,6 +181,7 @@ struct dice_batch {
     int64_t prune_waves = 0;        // waves of that launch (entries of d_nscored)
     int64_t surv_waves = 0;         // waves of the survivors kernel after it (the next entries)
     int32_t last_match = 0;         // last match call: 0 none, 1 every pair scored, 2 bound-pruned
+    int64_t n_long = 0;             // files of the upload with |W_F| above every template's |Lf| (-1: unknown)
     // Exact matcher (dice_batch_exact, lazily allocated): per-file result, field masks
     int32_t* d_exact = nullptr;
     uint64_t* d_fmask = nullptr;

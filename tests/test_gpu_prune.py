@@ -227,3 +227,42 @@ def test_batch_match_is_asynchronous_and_capturable():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert 'async ok' in r.stdout and 'capture ok' in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize('route', ['4', '0'])
+def test_long_file_batches_route_to_postings_in_match(route, monkeypatch):
+    """dice_match on a batch of long/mixed files (SyntheticCorpus profile 1: 2-6 templates plus
+    notices; 72% have more words than the largest template) goes to the postings kernels whole
+    (DICE_PRUNE_LONG_ROUTE, default 4: when at least a quarter of the files are long; 0: never),
+    while Dice#confidence keeps the pruned kernel; every result equals the oracle's either way, and
+    a batch of config-3 files stays on the pruned kernel."""
+    import bench
+    from licensee_amd.synth import SyntheticCorpus
+    monkeypatch.setenv('DICE_PRUNE_LONG_ROUTE', route)
+    c = bench.build_workload(3)
+    T = len(c.templates)
+    orc = _oracle(c)
+    sc = _scorer(c)
+    try:
+        for profile, n in ((1, 3000), (0, 3000)):
+            fb = SyntheticCorpus(c, profile=profile).generate(0, n, seed=7 + profile, nthreads=16)
+            b = sc.batch(n)
+            try:
+                b.upload(fb)
+                for thr in (98.0, 0.0):
+                    exp = orc.match(fb.bits, fb.wordset_size, fb.length, fb.cc_false_positive, thr, nthreads=16, mode=0)
+                    b.match(thr)
+                    _assert_same(b.download_match(), exp, ('match', profile, route, thr))
+                    routed = b.scored_pairs() == n * T
+                    assert routed == (profile == 1 and route != '0'), (profile, route, b.scored_pairs())
+                    b.match(thr, confidence=True)
+                    best, ov, score = b.download_match()
+                    hit = exp[0] >= 0
+                    assert np.array_equal(best, exp[0])
+                    assert np.array_equal(ov, np.where(hit, exp[1], 0)) and np.array_equal(score, np.where(hit, exp[2], 0.0))
+                    if thr == 98.0:
+                        assert b.scored_pairs() < n * T   # the confidence entry point stays pruned
+            finally:
+                b.close()
+    finally:
+        sc.close()
