@@ -76,6 +76,10 @@ __host__ __device__ __forceinline__ int32_t u8_row_words(int32_t tp) { return (t
 #endif
 // The walk's padding entries go to per-lane sinks instead of exec-masked adds (count_or_sink; 0:
 // the masked form, A/B)
+// the walk's entries 12-15 behind their own ballot (A/B)
+#ifndef POST_WALK_SPLIT12
+#define POST_WALK_SPLIT12 0
+#endif
 #ifndef POST_WALK_SINK
 #define POST_WALK_SINK 1
 #endif
@@ -213,8 +217,18 @@ __device__ __forceinline__ void walk_short(const uint32_t* wq, uint32_t nq, uint
         for (int k = 0; k < 8; ++k) count_or_sink(cbase, sink, (rr[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
         if (__ballot(mid)) {   // entries 8-15 (0xFFFF padding / the long marker for other words: sinks)
             const uint32_t r2[4] = {r1.x, r1.y, r1.z, r1.w};
+#if POST_WALK_SPLIT12
+            // entries 12-15 only when a lane's word has more than 12 (about two passes in three)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) count_or_sink(cbase, sink, (r2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+            if (__ballot(mid && (r1.z & 0xFFFFu) != kNoTpl)) {
+#pragma unroll
+                for (int k = 4; k < 8; ++k) count_or_sink(cbase, sink, (r2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+            }
+#else
 #pragma unroll
             for (int k = 0; k < 8; ++k) count_or_sink(cbase, sink, (r2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+#endif
         }
 #else
         const uint32_t rr[4] = {r0.x, r0.y, r0.z, r0.w};
