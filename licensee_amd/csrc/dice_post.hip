@@ -15,8 +15,9 @@
 //
 // Two kernels per launch:
 //   dice_post_dense_mfma (default): the files' first D u64 words against the template masks as a
-//            binary matrix product on the matrix cores (int8 MFMA, persistent workgroups; see
-//            below), written as a row-major [n][tp] u16 matrix; dice_post_dense (DICE_POST_MFMA=0,
+//            binary matrix product on the matrix cores (FP4 block-scaled MFMA, or int8 with
+//            DICE_POST_MFMA=1; persistent workgroups; see below), written as a row-major [n][tp]
+//            u16 matrix; dice_post_dense (DICE_POST_MFMA=0,
 //            lanes = files, 16 waves per 64-file tile): the same by v_bcnt, template masks by
 //            scalar loads, through an LDS [file][template] u16 stage;
 //   dice_post_narrow_{match,matrix} (one file per wave): the file's dense partials, widened,
@@ -360,24 +361,26 @@ __global__ __launch_bounds__(kPostWaves * kWave) __attribute__((amdgpu_waves_per
     }
 }
 
-// The dense prefix on the matrix cores (dice_post_dense_mfma, DICE_POST_MFMA, default 1). The
-// prefix overlap |W_F ∩ Lf_t ∩ prefix| is a binary matrix product -- files x prefix bits times
-// prefix bits x templates -- so with bits widened to int8 0/1, v_mfma_i32_32x32x32_i8 computes a
-// 32-file x 32-template tile 32 bits at a time, exactly (counts <= 1024). A persistent workgroup
+// The dense prefix on the matrix cores (dice_post_dense_mfma; DICE_POST_MFMA: 4 = FP4, the
+// default, 1 = int8). The prefix overlap |W_F ∩ Lf_t ∩ prefix| is a binary matrix product -- files
+// x prefix bits times prefix bits x templates -- so with bits widened to 0/1 operands an MFMA
+// computes a 32-file x 32-template tile exactly: v_mfma_i32_32x32x32_i8 32 bits at a time, the
+// FP4 v_mfma_scale_f32_32x32x64_f8f6f4 a whole u64 word (below; counts <= 1280, exact in f32). A persistent workgroup
 // (one per CU) = NW waves over tiles of MT x 32 files (MT = 3 for T <= 640, else 2); wave w owns
 // 1-2 N-tiles of 32 templates (the ceil(T / 32) tiles dealt so the SIMDs' shares differ by at
 // most one; 12 waves at 3 per SIMD, 11 above 640 templates), and each template fragment serves
 // the MT M-tiles. Per u64 prefix word q: the files' words from the LDS-staged prefixes, the
-// templates' words from the word-major masks (staged in LDS once per workgroup), each lane's 16
-// bits of a k-step widened to 16 bytes (widen_half: two VALU per dword), then MT x NTW MFMAs per
-// k-step. A and B place the same bit in the same fragment element, so the products pair the same
+// templates' words from the word-major masks (staged in LDS once per workgroup; FP4: as low/high
+// u32 planes), each lane's bits widened to the operand format (widen_half / widen_a, widen_b),
+// then MT x NTW MFMAs per word or k-step. A and B place the same bit in the same fragment element, so the products pair the same
 // bits whatever the hardware's k order inside a step. Accumulator register g of lane (h, c) is
-// file 32 m + (g & 3) + 8 (g >> 2) + 4 h, template 32 j + c: transposed through a per-wave LDS
-// slab and stored as 16-byte pieces of the [n][tp] u16 partial rows (a wave's 64 templates of one
-// file are 128 contiguous bytes). The next tile's prefixes are loaded into registers while this
-// tile is scored (LDS waits count lgkmcnt, so they fly across the tile) and written to LDS after
-// it. (5-T600 dense kernel, step by step: 1.70 ms -> 0.68 ms, the VALU kernel 1.45;
-// profiles/r4_mfma_dense.txt.)
+// file 32 m + (g & 3) + 8 (g >> 2) + 4 h, template 32 j + c: transposed through a per-wave 16 x 64
+// LDS slab and stored as 16-byte pieces of the [n][tp] u16 partial rows (a wave's 64 templates of
+// one file are 128 contiguous bytes). The next tile's prefixes are loaded into registers while
+// this tile is scored (LDS waits count lgkmcnt, so they fly across the tile) and written to the
+// other LDS buffer before this tile's stores are issued (one barrier per tile). (5-T600 dense
+// kernel: round 4 1.70 -> 0.68 ms, the VALU kernel 1.45, profiles/r4_mfma_dense.txt; round 5 FP4
+// 0.58, then 0.46 ms, profiles/r5_dense_ab.txt.)
 // timing splits only (tools/build_variant.sh -DPOST_DENSE_AB=n; results wrong): 1 = no partial
 // stores, 2 = no k-loop, 3 = no store phase (no slab, no stores)
 #ifndef POST_DENSE_AB
