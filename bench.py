@@ -440,6 +440,33 @@ def measure_extra(r, c, args, stream, sptr, cpu, group):
     return rec
 
 
+def collective_gather_leg(res, host_dst, group, rank, reps, sync):
+    """The collective form of the result gather: every rank's packed [n, 4] int32 results
+    (licensee_amd.shard.pack_results layout) to rank 0 with dist.gather, then one copy into rank
+    0's host buffer `host_dst` ([world * n, 4], shard order). Timed from a barrier, median of
+    `reps`, max over ranks; returns seconds. `sync` drains the device (torch.cuda.synchronize with
+    RCCL; a no-op for host tensors over gloo, which tests/test_distributed.py drives)."""
+    from licensee_amd.shard import gather_packed_to0
+    tr = []
+    for _ in range(reps):
+        sync()
+        group.barrier()
+        t0 = time.perf_counter()
+        g = gather_packed_to0(res)
+        if rank == 0:
+            host_dst.copy_(g)
+        sync()
+        group.barrier()
+        tr.append(time.perf_counter() - t0)
+    return group.reduce([float(np.median(tr))], 'max')[0]
+
+
+def gather_winner(host_s, rccl_s):
+    """The faster result gather (north_star: RCCL solely for the gather, or the host gather if it
+    proves faster); ties go to the host gather."""
+    return 'host' if host_s <= rccl_s else 'rccl'
+
+
 def gather_compare(batch, group, rank, world, n_per, best, ov, score, sptr, reps=3):
     """The one result move of a sharded run, two ways, both ending with every rank's 16-B/file
     results in rank 0's host memory (north_star: RCCL solely for the gather, or a host gather if
@@ -453,7 +480,7 @@ def gather_compare(batch, group, rank, world, n_per, best, ov, score, sptr, reps
     import torch
     import torch.distributed as dist
     from licensee_amd._native import _check, _ptr, load_library
-    from licensee_amd.shard import SharedResults, gather_packed_to0, device_results_packed, pack_results
+    from licensee_amd.shard import SharedResults, device_results_packed, pack_results
     lib = load_library()
     name = f"licensee_bench_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
     shared = SharedResults(name, world, n_per, create=True) if rank == 0 else None
@@ -493,20 +520,9 @@ def gather_compare(batch, group, rank, world, n_per, best, ov, score, sptr, reps
         if group.backend == 'nccl':
             res = device_results_packed(batch)
             host_dst = torch.empty((world * n_per, 4), dtype=torch.int32, pin_memory=True) if rank == 0 else None
-            tr = []
-            for _ in range(reps):
-                torch.cuda.synchronize()
-                group.barrier()
-                t0 = time.perf_counter()
-                g = gather_packed_to0(res)
-                if rank == 0:
-                    host_dst.copy_(g)
-                torch.cuda.synchronize()
-                group.barrier()
-                tr.append(time.perf_counter() - t0)
-            rccl_s = group.reduce([float(np.median(tr))], 'max')[0]
+            rccl_s = collective_gather_leg(res, host_dst, group, rank, reps, torch.cuda.synchronize)
             out['rccl_gather_ms'] = rccl_s * 1e3
-            out['gather_winner'] = 'host' if host_s <= rccl_s else 'rccl'
+            out['gather_winner'] = gather_winner(host_s, rccl_s)
             if rank == 0:
                 ref = pack_results(shared.best, shared.overlap, shared.score)
                 out['gather_agree'] = bool(np.array_equal(host_dst.numpy(), ref))
@@ -568,10 +584,17 @@ def abi_sharded_leg(run, args, n_dev, reps=3):
             mism = int(np.sum(outs[0] != eb) + np.sum(outs[1] != eo) + np.sum(outs[2] != es))
             rec[name] = {'ms_per_call': ms, 'files_per_s': n / (ms * 1e-3), 'mismatches': mism,
                          'dice_last_gather_peer': last_gather_peer()}
-        rec['winner'] = 'host' if rec['host']['ms_per_call'] <= rec['device']['ms_per_call'] else 'device'
+        distinct = len(set(devices))
+        if distinct >= 2:
+            rec['winner'] = 'host' if rec['host']['ms_per_call'] <= rec['device']['ms_per_call'] else 'device'
+        else:
+            # every context on one device: the device gather moves nothing between devices, so the
+            # two timings are no evidence about xGMI
+            rec['winner'] = None
+            rec['winner_reason'] = f'{distinct} distinct device(s): no cross-device gather to compare'
         rec['note'] = ('PCIe-inclusive (inputs start in host memory, as the FFI hands them over); the kernel-only rate '
                        'is `value`. dice_last_gather_peer: 1 = every remote shard written over xGMI peer access, '
-                       '0 = some staged, -1 = host gather')
+                       '0 = some staged, -1 = no peer path exercised (host gather, or every context on one device)')
     finally:
         for sc in scorers:
             sc.close()

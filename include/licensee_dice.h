@@ -154,9 +154,9 @@ int dice_similarity_matrix_sharded(dice_ctx *const *ctxs, int32_t n_ctx, const d
                                    int32_t gather_mode, uint32_t *overlap, double *score, int32_t k,
                                    int32_t *topk_index, double *topk_score);
 /* The last sharded call on this thread: 1 = device gather, every shard on another device wrote
- * into ctxs[0]'s device through peer access (shards on ctxs[0]'s own device count as local);
- * 0 = device gather with at least one shard through the runtime's staged copy; -1 = host
- * gather or no sharded call yet. */
+ * into ctxs[0]'s device through peer access; 0 = device gather with at least one such shard
+ * through the runtime's staged copy; -1 = no peer path exercised: a host gather, a device gather
+ * whose contexts all sit on ctxs[0]'s device, or no sharded call yet. */
 int32_t dice_last_gather_peer(void);
 
 /* ---- device-resident batches (inputs and results stay in HBM) ---------------------- */

@@ -512,7 +512,8 @@ def match_sharded(scorers, files: FileBatch, threshold: float, gather: int = DIC
 
 def last_gather_peer() -> int:
     """``dice_last_gather_peer``: 1 when the last sharded call's device gather wrote every remote
-    shard through peer access, 0 when some went through a staged copy, -1 for a host gather."""
+    shard through peer access, 0 when some went through a staged copy, -1 when no peer path was
+    exercised (a host gather, or every context on the first context's device)."""
     return int(load_library().dice_last_gather_peer())
 
 

@@ -319,9 +319,8 @@ static void ctx_free(dice_ctx* c) {
     if (c->d_tq) (void)hipFree(c->d_tq);
     if (c->d_tc) (void)hipFree(c->d_tc);
     if (c->d_qperm) (void)hipFree(c->d_qperm);
-    void* plan[] = {c->d_lrec, c->d_lep,  c->d_les,  c->d_lwt,   c->d_pdmt, c->d_prow,  c->d_povf, c->d_pdm,
-                    c->d_ptc,  c->d_p4q8, c->d_p4tc, c->d_p4cc,  c->d_p4off, c->d_p4rec, c->d_p4slot,
-                    c->d_p4q32, c->d_p4s32};
+    void* plan[] = {c->d_lrec, c->d_lep,  c->d_les,  c->d_lwt,   c->d_pdmt,  c->d_prow,  c->d_povf,
+                    c->d_ptc,  c->d_p4q8, c->d_p4tc, c->d_p4cc,  c->d_p4off, c->d_p4rec, c->d_p4slot};
     for (void* p : plan)
         if (p) (void)hipFree(p);
     if (c->module) (void)hipModuleUnload(c->module);
@@ -490,7 +489,7 @@ void dice_batch_destroy(dice_batch* b) {
     }
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
                     b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
-                    b->d_defer, b->d_ndefer, b->d_nscored, b->d_qctr, b->d_exact, b->d_fmask};
+                    b->d_defer, b->d_ndefer, b->d_nscored, b->d_exact, b->d_fmask};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -563,6 +562,7 @@ int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
     hipStream_t s = pick_stream(c, stream);
     const int64_t n = f->n_files;
     b->n = n;
+    b->n_long = 0;
     if (n == 0) return DICE_OK;
     HIP_TRY(hipMemcpyAsync(b->d_rows, f->bits, (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, s));
     return upload_tail(b, n, f->wordset_size, f->length, f->cc_false_positive, s);
@@ -576,6 +576,7 @@ int dice::upload_rows_resident(dice_batch* b, const dice_files* f, hipStream_t s
     if (f->n_files < 0 || f->n_files > b->capacity) return fail(DICE_E_ARG, "n_files exceeds batch capacity");
     DeviceGuard g(b->ctx->device);
     b->n = f->n_files;
+    b->n_long = 0;
     if (b->n == 0) return DICE_OK;
     return upload_tail(b, b->n, f->wordset_size, f->length, f->cc_false_positive, s);
 }
@@ -599,6 +600,7 @@ int dice_batch_upload_ids(dice_batch* b, int64_t n, const int64_t* offsets, cons
     DeviceGuard g(c->device);
     hipStream_t s = pick_stream(c, stream);
     b->n = n;
+    b->n_long = 0;
     if (n == 0) return DICE_OK;
     const size_t need = (size_t)std::max<int64_t>(offsets[n], 1) * (size_t)id_bytes;
     if (need > b->ids_bytes) {
@@ -645,7 +647,10 @@ __global__ __launch_bounds__(256) void dice_confidence_outputs(const int32_t* __
 static int batch_match(dice_batch* b, double thr, void* stream, bool confidence) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
     dice_ctx* c = b->ctx;
-    if (b->n == 0) return DICE_OK;
+    if (b->n == 0) {
+        b->last_match = 1;   // every pair of the empty batch scored: n * T = 0, nothing deferred
+        return DICE_OK;
+    }
     DeviceGuard g(c->device);
     hipStream_t s = pick_stream(c, stream);
     const int64_t n_tiles = (b->n + kWave - 1) / kWave;
@@ -819,14 +824,15 @@ int dice_batch_stream_probe(dice_batch* b, void* stream) {
 int dice_batch_deferred(dice_batch* b, int64_t* deferred, void* stream) {
     if (!b || !deferred) return fail(DICE_E_ARG, "NULL batch/output");
     *deferred = 0;
-    if (!b->d_ndefer || !b->ctx->prune) return DICE_OK;
+    // only the bound-pruned match defers files (dice_match may route a batch of long files to the
+    // postings kernels instead: the count of an earlier pruned call is then stale)
+    if (!b->d_ndefer || !b->ctx->prune || b->last_match != 2) return DICE_OK;
     DeviceGuard g(b->ctx->device);
-    uint32_t m[2] = {0, 0};
+    uint32_t m = 0;
     hipStream_t s = pick_stream(b->ctx, stream);
-    HIP_TRY(hipMemcpyAsync(m, b->d_ndefer, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&m, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    // the files that reached the postings kernels: after the survivors kernel when it ran
-    *deferred = b->surv_waves ? m[1] : m[0];
+    *deferred = m;
     return DICE_OK;
 }
 
@@ -841,15 +847,15 @@ int dice_batch_scored_pairs(dice_batch* b, int64_t* pairs, void* stream) {
         // (the postings kernels score them all)
         DeviceGuard g(c->device);
         hipStream_t s = pick_stream(c, stream);
-        // (dice_prune4's waves, then the survivors kernel's; the files the postings kernels scored)
-        const int64_t nw = b->prune_waves + b->surv_waves;
-        std::vector<uint32_t> h((size_t)nw + 2);
+        // (dice_prune4's per-wave counts, then the number of files the postings kernels scored)
+        const int64_t nw = b->prune_waves;
+        std::vector<uint32_t> h((size_t)nw + 1);
         HIP_TRY(hipMemcpyAsync(h.data(), b->d_nscored, (size_t)nw * 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(h.data() + nw, b->d_ndefer, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h.data() + nw, b->d_ndefer, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         int64_t sum = 0;
         for (int64_t i = 0; i < nw; ++i) sum += h[(size_t)i];
-        *pairs = sum + (int64_t)h[(size_t)nw + (b->surv_waves ? 1 : 0)] * c->T;
+        *pairs = sum + (int64_t)h[(size_t)nw] * c->T;
     }
     return DICE_OK;
 }

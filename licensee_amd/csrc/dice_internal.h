@@ -75,16 +75,12 @@ struct dice_ctx {
     int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1, lds_wide = 0, lds_tiles = 2;
     int64_t lds_entries = 0;
     // kind 3 plan (dice_post.hip): postings rows of the narrow words, dense-prefix masks
-    void* d_pdmt = nullptr;    // [16][kMfmaCols] u64 dense-prefix masks, word-major, zero-padded (MFMA kernel)
+    void* d_pdmt = nullptr;    // [20][kMfmaCols] u64 dense-prefix masks, word-major, zero-padded (MFMA kernel)
     void* d_prow = nullptr;    // [64*w64][16] u16 postings row per word (short ids / long word ref)
     void* d_povf = nullptr;    // flat u16 template ids of the long words
-    void* d_pdm = nullptr;     // [T][16] u64 dense-prefix masks
     void* d_ptc = nullptr;     // [T] int4 template constants
     int32_t post_dense = 0, post_tpad = 0, post_tp = 0, post_ld = 0;
     bool post_fast = false;
-    int32_t post_mfma = 4;     // dense prefix: 4 dice_post_dense_mfma FP4 (default), 1 its int8 form, 0 the VALU kernel (DICE_POST_MFMA)
-    int32_t post_u8 = 0;       // FP4 dense kernel: u8 partial rows for files with <= 255 prefix words (DICE_POST_U8=1, A/B; slower)
-    int32_t post_mfma_mt = 3;  // 32-file M-tiles per MFMA tile (T <= 640; DICE_POST_MFMA_MT=2 for A/B)
     int64_t post_rows = 0;
     // kind 3 match mode, bound-pruned (dice_prune.hip): tables in position (length-sorted) order --
     // group bytes, constants, CC masks, template index | record offset, records, slot bounds
@@ -93,8 +89,7 @@ struct dice_ctx {
     int32_t prune_long_route = 4;    // dice_match: postings kernels when >= 1/N of a batch's files are long (0: never)
     uint32_t prune_wf_noclamp = 0;   // |W_F| from which the bound's length term needs no clamp
     void *d_p4q8 = nullptr, *d_p4tc = nullptr, *d_p4cc = nullptr, *d_p4off = nullptr, *d_p4rec = nullptr,
-         *d_p4slot = nullptr, *d_p4q32 = nullptr, *d_p4s32 = nullptr;
-    int32_t prune_surv_evals = 0;    // survivors kernel: exact scores per file before the postings kernels (0: off)
+         *d_p4slot = nullptr;
     int32_t p4_zkeep[2] = {-1, -1}, p4_zpos[2] = {0, 0};
     int32_t n_cu = 256, prune_max_evals = 8, prune_route = 16;
     // sharded calls (dice_shard.cpp): devices this ctx's device has peer access to (bit d), and
@@ -174,12 +169,10 @@ struct dice_batch {
     size_t pdense_bytes = 0;
     size_t stage_bytes = 0;
     // pruned match (dice_prune.hip): files deferred to the postings kernels
-    int32_t* d_defer = nullptr;     // [2][capacity] file indices: dice_prune4's deferred files, the survivors kernel's
-    uint32_t* d_ndefer = nullptr;   // [2] their counts
-    uint32_t* d_qctr = nullptr;     // sparse-program tile-queue counters (DICE_PROG_QUEUE A/B)
+    int32_t* d_defer = nullptr;     // [capacity] file indices dice_prune4 deferred
+    uint32_t* d_ndefer = nullptr;   // their count
     uint32_t* d_nscored = nullptr;  // per wave of the last pruned launch: (file, template) pairs scored exactly
     int64_t prune_waves = 0;        // waves of that launch (entries of d_nscored)
-    int64_t surv_waves = 0;         // waves of the survivors kernel after it (the next entries)
     int32_t last_match = 0;         // last match call: 0 none, 1 every pair scored, 2 bound-pruned
     int64_t n_long = 0;             // files of the upload with |W_F| above every template's |Lf| (-1: unknown)
     // Exact matcher (dice_batch_exact, lazily allocated): per-file result, field masks

@@ -162,60 +162,6 @@ extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_mat
 }
 )HIP";
 
-// Tile-queue match kernel (DICE_PROG_QUEUE=8 or 1; A/B only -- the default source text stays the
-// kernel above): a grid of resident waves, each taking its next 64-file tile from one of QGROUPS
-// counters (group = blockIdx % QGROUPS; with 8, the workgroups sharing an XCD, since blocks are
-// dealt round-robin over the 8 XCDs), group g owning tiles [n_tiles g / QG, n_tiles (g + 1) / QG).
-// The next tile is requested before the current one is scored; every wave ends with exactly one
-// claim past its group's range, so the wave whose claim is the group's last resets that counter
-// for the next launch (no memset, capturable). Round 4 measured ONE counter 3x slower (15.6k
-// same-address atomics serialize); QGROUPS spreads them over 8 addresses.
-const char* kMatchKernelQueue = R"HIP(
-extern "C" __global__ __launch_bounds__(64 * WPB MATCH_WAVES) void dice_prog_match(
-    const uint4* __restrict__ files, i64 n, const u32* __restrict__ wfp, const i32* __restrict__ lenp,
-    const unsigned char* __restrict__ ccp, double thr, i32* __restrict__ best_out,
-    u32* __restrict__ ov_out, double* __restrict__ score_out, u32* __restrict__ qctr) {
-    const int lane = threadIdx.x & 63;
-    const u32 n_tiles = (u32)((n + 63) >> 6);
-    const u32 g = blockIdx.x % QGROUPS;
-    const u32 lo = (u32)(((u64)n_tiles * g) / QGROUPS), hi = (u32)(((u64)n_tiles * (g + 1)) / QGROUPS);
-    const u32 groups_g = (gridDim.x - g + QGROUPS - 1) / QGROUPS;   // blocks b < gridDim.x with b % QG == g
-    const u32 last = (hi - lo) + groups_g * WPB - 1;
-    u32* ctr = qctr + g * 32;                                          // counters 128 B apart
-    u32 got = 0;
-    if (lane == 0) got = atomicAdd(ctr, 1u);
-    u32 k = __builtin_amdgcn_readfirstlane(got);
-    while (k < hi - lo) {
-        u32 nx = 0;
-        if (lane == 0) nx = atomicAdd(ctr, 1u);
-        const i64 tile = (i64)(lo + k);
-        const i64 file = tile * 64 + lane;
-        const uint4* fp = files + tile * (i64)(WQ * 64) + lane;
-        const u32 wf = wfp[file];
-        const i32 lf = lenp[file];
-        const bool cc = ccp[file] != 0;
-        FILE_PROLOGUE
-        const bool fast = CORPUS_FAST && wf < (1u << 20) && lf >= 0 && lf < (1 << 21);
-        u32 bo = 0xFF000000u; i32 bd = 1;
-        if (__all(fast)) {
-            MATCH_BODY(true)
-        } else {
-            MATCH_BODY(false)
-        }
-        if (file < n) {
-            const i32 bi = (bo >> 24) == 0xFFu ? -1 : (i32)(bo >> 24);
-            const u32 bov = bo & 0xFFFFFFu;
-            const double s = bi >= 0 ? sc(bov, bd) : 0.0;
-            MSTORE(best_out + file, (bi >= 0 && s >= thr) ? bi : -1);
-            MSTORE(ov_out + file, bov);
-            MSTORE(score_out + file, s);
-        }
-        k = __builtin_amdgcn_readfirstlane(nx);
-    }
-    if (k == last && lane == 0) atomicExch(ctr, 0u);
-}
-)HIP";
-
 // Matrix kernel template: KM is the compile-time top-k slot count (4 or 16).
 const char* kMatrixKernel = R"HIP(
 extern "C" __global__ __launch_bounds__(64 * WPB) void KNAME(
@@ -633,8 +579,7 @@ std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool
         match_body.str(mb.str());
     }
     emit_macro(s, "MATCH_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", match_body.str() + "}");
-    if (p.queue) s << "#define QGROUPS " << p.queue << "\n";
-    s << "#define ACC_INIT(i) ((u32)(i) << 24)\n" << (p.queue ? kMatchKernelQueue : kMatchKernel)
+    s << "#define ACC_INIT(i) ((u32)(i) << 24)\n" << kMatchKernel
       << "#undef ACC_INIT\n#define ACC_INIT(i) 0u\n";
     s << kMatrixOffer;
     emit_macro(s, "MATRIX_BODY(FASTV_) { constexpr bool FASTV = FASTV_;", matrix_body.str() + "}");
@@ -711,8 +656,6 @@ static std::string source_for(const dice_templates* t, Program& prog) {
     build_entries(t, w64, prog);
     const char* wpb = getenv("DICE_PROG_WPB");   // waves per workgroup (A/B runs; default 4)
     prog.wpb = wpb && *wpb ? std::max(1, std::min(16, atoi(wpb))) : 4;
-    const char* q = getenv("DICE_PROG_QUEUE");   // match kernel: tile queue with 1 or 8 counters (A/B)
-    prog.queue = q && (*q == '1' || *q == '8') ? atoi(q) : 0;
     return program_source(t, prog, (w64 + 1) / 2, corpus_in_fast_envelope(t));
 }
 
@@ -734,16 +677,6 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
         if (hipMemcpy(c->d_qperm, c->prog.qperm.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
             return fail(DICE_E_DEVICE, "program tile permutation upload failed");
     }
-    if (c->prog.queue) {
-        int per_cu = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->prog_match, 64 * c->prog.wpb, 0) !=
-                hipSuccess || per_cu < 1)
-            return fail(DICE_E_DEVICE, "occupancy query for dice_prog_match failed");
-        int n_cu = 0;
-        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || n_cu < 1)
-            n_cu = 256;
-        c->prog.resident_groups = (int64_t)per_cu * n_cu;
-    }
     c->kind = 1;
     return DICE_OK;
 }
@@ -751,21 +684,10 @@ int program_setup(dice_ctx* c, const dice_templates* t) {
 int program_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + 63) / 64;
     const int32_t wpb = c->prog.wpb;
-    int64_t groups = (n_tiles + wpb - 1) / wpb;
-    if (c->prog.queue) {
-        // resident waves only (at least one workgroup per counter group); counters per batch, zeroed once
-        if (!b->d_qctr) {
-            int rc = dalloc_bytes(reinterpret_cast<void**>(&b->d_qctr), 8 * 128);
-            if (rc) return rc;
-            if (hipMemset(b->d_qctr, 0, 8 * 128) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemset failed");
-        }
-        groups = std::max<int64_t>(std::min(groups, c->prog.resident_groups), c->prog.queue);
-    }
-    const unsigned grid = (unsigned)groups;
+    const unsigned grid = (unsigned)((n_tiles + wpb - 1) / wpb);
     hipFunction_t fn = c->prog_match;
     int64_t n = b->n;
-    void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score, &b->d_qctr};
-    (void)args[9];   // (the queue kernel's extra argument; the default kernel takes the first nine)
+    void* args[] = {&b->d_tiles, &n, &b->d_wf, &b->d_len, &b->d_cc, &thr, &b->d_best, &b->d_ov, &b->d_score};
     if (hipModuleLaunchKernel(fn, grid, 1, 1, 64 * wpb, 1, 1, 0, s, args, nullptr) != hipSuccess)
         return fail(DICE_E_DEVICE, "launch dice_prog_match failed");
     return DICE_OK;

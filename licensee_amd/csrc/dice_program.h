@@ -23,8 +23,6 @@ struct Program {
     std::vector<int32_t> dword_map;   // vocab dword -> file dword in the remapped layout (-1: unused)
     int32_t wpb = 4;                  // waves (64-file tiles) per workgroup
     std::vector<int32_t> qperm;       // tile slot -> vocabulary quad (empty: identity)
-    int32_t queue = 0;                // match kernel tile-queue counters (0: one tile per wave; A/B)
-    int64_t resident_groups = 0;      // workgroups resident at once (queue mode)
     size_t entries() const { return prog.size(); }
 };
 

@@ -35,7 +35,6 @@
 namespace dice {
 
 constexpr int kPruneWaves = 16;          // waves per workgroup
-constexpr int kSurvWaves = 8;            // waves per workgroup of the survivors kernel
 constexpr int kPruneGroups = 16;         // word groups of the bound
 constexpr int kPruneMaxJ = 8;            // u64 words per lane: w64 <= 512 (V <= 32768)
 constexpr int kPruneMaxT = 704;          // = kPostMaxTpad (the key's low 10 bits hold the template)
@@ -518,184 +517,6 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(8, 8
 }
 
 
-// ---- survivors: the deferred files with a finer bound -------------------------------------
-//
-// A file dice_prune4 defers still has many templates whose 16-group bound reaches its best score
-// (heavily perturbed texts, stacked licenses): the bound is loose, not the file unusual. Before
-// round 5 every such file went to the postings kernels, which score all T pairs (~4% of the
-// config-3 files, ~0.19 of 0.90 ms through dice_batch_match). This kernel takes them from the
-// device list and bounds them again with 32 word groups (word p in group (p mod 64) / 2: a lane
-// pair) -- twice the resolution, computed only for these files, so the match kernel keeps its
-// 64-VGPR budget (round 3 measured 32 groups inside dice_prune4: slower, spills) -- then scores
-// the largest keys exactly as dice_prune4 does, in the same strict (score, later key) order and
-// with the same f32 margin, so best / overlap / score equal the full scan's. A file that still
-// needs more than max_evals exact scores (or leaves the plain range) goes on to the postings
-// kernels through a second device list.
-//
-// Tables (position order, as dice_prune4): q32 = the 32 group counts clamped to a byte (two uint4
-// per template; safe as for 16 groups: a file whose group count exceeds 255 uses the 2 |W_F ∩ V|
-// bound), s32 = their sum; stc / ccm / srec / qrec shared with dice_prune4.
-template <int J, int TJ, int NW>
-__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4, 4))) void dice_prune_survivors(
-    const uint64_t* __restrict__ rows, int32_t w64, int32_t T, Prune4Args pa, const uint4* __restrict__ q32g,
-    const uint32_t* __restrict__ s32g, const uint32_t* __restrict__ wfp, const int32_t* __restrict__ lenp,
-    const uint8_t* __restrict__ ccp, double thr, int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out,
-    double* __restrict__ score_out, bool corpus_fast, bool zero_base, const int32_t* __restrict__ defer,
-    const uint32_t* __restrict__ ndefer, int32_t* __restrict__ defer2, uint32_t* __restrict__ ndefer2,
-    int32_t max_evals, float llo0, bool conf, uint32_t* __restrict__ nscored) {
-    constexpr int kTP = TJ * kWave;
-    constexpr int J2 = (J + 1) / 2;
-    // LDS: [kTP][2] uint4 32-group bytes | [kTP] uint4 constants | [kTP] cc masks | [kTP] 32-group
-    // sums | [kTP + 1] template index | record offset << 10 | the waves' rows
-    extern __shared__ uint64_t lds[];
-    uint4* q32 = reinterpret_cast<uint4*>(lds);
-    uint4* stc = q32 + 2 * kTP;
-    uint32_t* ccm = reinterpret_cast<uint32_t*>(stc + kTP);
-    uint32_t* s32 = ccm + kTP;
-    uint32_t* srec = s32 + kTP;
-    uint64_t* rows0 = lds + (((size_t)kTP * (32 + 16 + 4 + 4) + ((size_t)kTP + 1) * 4 + 15) / 16) * 2;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = (int)rfl(threadIdx.x >> 6);
-    uint64_t* myrow = rows0 + (size_t)wave * J2 * 2 * kWave;
-    for (int i = threadIdx.x; i < kTP; i += NW * kWave) {
-        q32[2 * i] = q32g[2 * i];
-        q32[2 * i + 1] = q32g[2 * i + 1];
-        stc[i] = pa.tc[i];
-        ccm[i] = pa.ccm[i];
-        s32[i] = s32g[i];
-    }
-    for (int i = threadIdx.x; i <= kTP; i += NW * kWave) srec[i] = pa.srec[i];
-    __syncthreads();
-    const int64_t nn = (int64_t)*ndefer;
-    const int64_t gw = (int64_t)blockIdx.x * NW + wave, stride = (int64_t)gridDim.x * NW;
-    uint32_t nsc = 0;
-    // files this wave defers, one per lane (lane i: the i-th), flushed 64 at a time: one atomic per
-    // flush (per-file atomics on one counter serialize at ~11 ns each)
-    int32_t dq = 0;
-    uint32_t ndq = 0;
-    for (int64_t pos = gw; pos < nn; pos += stride) {   // wave-uniform
-        const int64_t file = (int64_t)(int32_t)rfl((uint32_t)defer[pos]);
-        uint4 w[J2];
-        row_load<J2>(w, rows, file, w64, lane);
-        const uint32_t wf = rfl(wfp[file]);
-        const int32_t lfi = (int32_t)rfl((uint32_t)lenp[file]);
-        const bool ccf = rfl(ccp[file]) != 0;
-        const uint32_t lf = (uint32_t)lfi;
-        bool deferred = lfi < 0 || wf >= (1u << 28) || (zero_base && wf == 0);
-        int32_t bi = -1, bd = 1;
-        uint32_t bo = 0;
-        __builtin_amdgcn_wave_barrier();   // the previous file's row reads are done (LDS ops run in order)
-        row_store<J2>(myrow, w, lane);
-        uint32_t pc = 0;
-#pragma unroll
-        for (int j = 0; j < J2; ++j)
-            pc += (uint32_t)__builtin_popcount(w[j].x) + (uint32_t)__builtin_popcount(w[j].y) +
-                  (uint32_t)__builtin_popcount(w[j].z) + (uint32_t)__builtin_popcount(w[j].w);
-        if (!deferred) {
-            // group g = lanes 2g, 2g + 1: the pair's sum in both lanes
-            const uint32_t pc2 = pc + (uint32_t)__builtin_amdgcn_mov_dpp((int)pc, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-            const bool big = __ballot(pc2 > 255u) != 0;
-            const uint32_t wv = rfl(__builtin_amdgcn_readlane(wave_incl_scan(pc), kWave - 1));
-            uint32_t fb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (!big) {
-                // dword k = groups 4k..4k+3 = the pair sums at lanes 8k, 8k+2, 8k+4, 8k+6, packed at lane 8k+6
-                uint32_t x = pc2 << 24;
-                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc2, 0x112, 0xf, 0xf, false) << 16;   // row_shr:2
-                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc2, 0x114, 0xf, 0xf, false) << 8;    // row_shr:4
-                x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pc2, 0x116, 0xf, 0xf, false);         // row_shr:6
-#pragma unroll
-                for (int k = 0; k < 8; ++k) fb[k] = rfl(__builtin_amdgcn_readlane(x, 8 * k + 6));
-            }
-            if (wv == 0) {
-                // (dice_prune4 resolves these itself; kept for a list written by another producer)
-                bi = pa.zkeep[ccf ? 1 : 0];
-                if (bi >= 0) bd = den3(stc[pa.zpos[ccf ? 1 : 0]], wf, lf);
-            } else {
-                const uint32_t wf4 = 4u * wf, negwv = 0u - wv;
-                const bool fast = corpus_fast && wf < (1u << 20) && lf < (1u << 21);
-                float llo = llo0;
-                uint32_t key[TJ], lmax = 0;
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) {
-                    const int32_t t = lane + j * kWave;
-                    const uint4 c = stc[t];
-                    uint32_t mm;
-                    if (!big) {
-                        const uint4 a = q32[2 * t], b = q32[2 * t + 1];
-                        uint32_t d = __builtin_amdgcn_sad_u8(a.x, fb[0], negwv);
-                        d = __builtin_amdgcn_sad_u8(a.y, fb[1], d);
-                        d = __builtin_amdgcn_sad_u8(a.z, fb[2], d);
-                        d = __builtin_amdgcn_sad_u8(a.w, fb[3], d);
-                        d = __builtin_amdgcn_sad_u8(b.x, fb[4], d);
-                        d = __builtin_amdgcn_sad_u8(b.y, fb[5], d);
-                        d = __builtin_amdgcn_sad_u8(b.z, fb[6], d);
-                        d = __builtin_amdgcn_sad_u8(b.w, fb[7], d);
-                        mm = s32[t] - d;
-                    } else {
-                        mm = 2u * wv;
-                    }
-                    const uint32_t x = (uint32_t)max((int32_t)__usad(c.x, lf, c.y), 0);
-                    const uint32_t d4 = c.z + wf4 + x;
-                    const float q = (float)mm * __builtin_amdgcn_rcpf((float)d4);
-                    uint32_t k = (__float_as_uint(q) & ~kKeyLow) | (uint32_t)(j + 1);
-                    if (ccf) k &= ~ccm[t];
-                    key[j] = t < T ? k : 0u;
-                    lmax = max(lmax, key[j]);
-                }
-                __builtin_amdgcn_wave_barrier();   // the row (written above) is read by other lanes below
-                if (__ballot(lmax != 0 && !(__uint_as_float(lmax) < llo)) != 0)
-                for (int32_t evals = 0;; ++evals) {
-                    uint32_t km = 0;
-#pragma unroll
-                    for (int j = 0; j < TJ; ++j) {
-                        if (__uint_as_float(key[j]) < llo) key[j] = 0;
-                        km = max(km, key[j]);
-                    }
-                    if (__ballot(km != 0) == 0) break;   // every template scored or dropped
-                    if (evals == max_evals) {
-                        deferred = true;
-                        break;
-                    }
-                    const uint32_t K = rfl(__builtin_amdgcn_readlane(wave_incl_max(km), kWave - 1));
-                    int32_t ls;
-                    const int32_t ts = key_template(K, km, ls);
-                    if (lane == ls) {
-#pragma unroll
-                        for (int j = 0; j < TJ; ++j)
-                            if (j == (ts >> 6)) key[j] = 0;
-                    }
-                    int32_t to;
-                    const RecHead h = records_head(ts, srec, pa.qrec, lane, to);
-                    score_template(ts, to, h, pa.qrec, myrow, stc, wf, lf, fast, lane, bi, bo, bd, llo);
-                    ++nsc;
-                }
-            }
-        }
-        if (deferred) {
-            if ((uint32_t)lane == ndq) dq = (int32_t)file;
-            if (++ndq == kWave) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(ndefer2, (uint32_t)kWave);
-                defer2[rfl(__builtin_amdgcn_readlane(base, 0)) + lane] = dq;
-                ndq = 0;
-            }
-        } else if (lane == 0) {
-            const double sc = bi >= 0 ? dice_score(bo, bd) : 0.0;
-            const bool hit = bi >= 0 && sc >= thr;
-            best_out[file] = hit ? bi : -1;
-            ov_out[file] = (conf && !hit) ? 0u : bo;
-            score_out[file] = (conf && !hit) ? 0.0 : sc;
-        }
-    }
-    if (ndq) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(ndefer2, ndq);
-        base = rfl(__builtin_amdgcn_readlane(base, 0));
-        if ((uint32_t)lane < ndq) defer2[base + lane] = dq;
-    }
-    if (lane == 0) nscored[gw] = nsc;
-}
-
 // ---- host side ---------------------------------------------------------------------------
 
 // templates per lane (ceil(T / 64) rounded to an instantiated width) and u64 row words per lane
@@ -718,14 +539,6 @@ static size_t prune_lds_bytes(int32_t nw, int32_t w64, int32_t T) {
 // files, 3 reps: 16 -> 0.845 ms, 32 -> 0.878, 64 -> 0.909; long/mixed files 2.08 / 2.13 / 2.12 ms
 // per 250k)
 constexpr int32_t kRouteCands = 16;
-// exact scores per deferred file in the survivors kernel before it goes on to the postings kernels;
-// 0 (default): no survivors kernel. Measured on config 3 through dice_batch_match (2 interleaved
-// reps, kernel trace in profiles/r5_survivors.txt): 0.95 ms with 32, 0.93 with 16, 0.886 without;
-// the kernel alone takes 157 / 129 / 102 us at 32 / 16 / 4 exact scores for the ~49k deferred files
-// -- each exact score reads a template's ~85 records from L2, so a file needing more than ~3 of
-// them costs more than the postings pass, which scores all 600 templates from ~220 postings rows.
-constexpr int32_t kSurvMaxEvals = 0;
-
 // The tables of dice_prune4, in position order (templates stably sorted by length): group bytes,
 // constants {length, -max(slack, 0), 4 base - 3, sum of group bytes}, CC masks, template index |
 // record offset << 10, the records {u64 word index, mask lo, mask hi, 0} of every nonzero u64
@@ -740,8 +553,7 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     std::vector<int32_t> pos2t((size_t)T);
     for (int32_t i = 0; i < T; ++i) pos2t[(size_t)i] = i;
     std::stable_sort(pos2t.begin(), pos2t.end(), [&](int32_t a, int32_t b) { return t->length[a] < t->length[b]; });
-    std::vector<uint32_t> q8p(tp * 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0), srec(tp + 1, 0), q32p(tp * 8, 0),
-        s32p(tp, 0);
+    std::vector<uint32_t> q8p(tp * 4, 0), ccp(tp, 0), offp((size_t)T + 1, 0), srec(tp + 1, 0);
     std::vector<uint4> tcp(tp, make_uint4(0, 0, 0, 0)), recp;
     bool zero_base = false;
     for (int32_t p = 0; p < T; ++p) {
@@ -759,17 +571,6 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
             sum8 += a8;
             q8p[(size_t)p * 4 + g / 4] |= a8 << (8 * (g % 4));
         }
-        // the survivors kernel's 32 groups (word w in group (w mod 64) / 2)
-        uint32_t g32[32] = {0};
-        for (int32_t w = 0; w < w64; ++w)
-            for (uint64_t x = r[w]; x; x &= x - 1) ++g32[(w % kWave) / 2];
-        uint32_t sum32 = 0;
-        for (int g = 0; g < 32; ++g) {
-            const uint32_t a8 = std::min<uint32_t>(g32[g], 255u);
-            sum32 += a8;
-            q32p[(size_t)p * 8 + g / 4] |= a8 << (8 * (g % 4));
-        }
-        s32p[(size_t)p] = sum32;
         const int32_t slack = t->length_slack[i];
         const uint32_t base = t->lf_size[i] - t->fields_set_size[i];   // post_feasible: 0 <= base < 2^16
         zero_base = zero_base || base == 0;
@@ -813,12 +614,8 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     int rc;
     if ((rc = dalloc_bytes(&c->d_p4q8, q8p.size() * 4)) || (rc = dalloc_bytes(&c->d_p4tc, tcp.size() * 16)) ||
         (rc = dalloc_bytes(&c->d_p4cc, ccp.size() * 4)) || (rc = dalloc_bytes(&c->d_p4off, srec.size() * 4)) ||
-        (rc = dalloc_bytes(&c->d_p4rec, recp.size() * 16)) || (rc = dalloc_bytes(&c->d_p4slot, slot.size() * 16)) ||
-        (rc = dalloc_bytes(&c->d_p4q32, q32p.size() * 4)) || (rc = dalloc_bytes(&c->d_p4s32, s32p.size() * 4)))
+        (rc = dalloc_bytes(&c->d_p4rec, recp.size() * 16)) || (rc = dalloc_bytes(&c->d_p4slot, slot.size() * 16)))
         return rc;
-    if (hipMemcpy(c->d_p4q32, q32p.data(), q32p.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->d_p4s32, s32p.data(), s32p.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-        return fail(DICE_E_DEVICE, "pruned-match plan upload failed");
     if (hipMemcpy(c->d_p4q8, q8p.data(), q8p.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_p4tc, tcp.data(), tcp.size() * 16, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_p4cc, ccp.data(), ccp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -847,11 +644,6 @@ int prune_setup(dice_ctx* c, const dice_templates* t) {
     // A/B: DICE_PRUNE_ROUTE_AT = exact scores before the routing test (default 2)
     const char* ra = getenv("DICE_PRUNE_ROUTE_AT");
     if (ra && *ra) c->prune_route |= std::min(std::max(1, atoi(ra)), 64) << 16;
-    // the survivors kernel (32-group bounds for the deferred files) and its exact-score limit per
-    // file (A/B: DICE_PRUNE_SURVIVORS=n; 0, the default, sends the deferred files straight to the
-    // postings kernels)
-    const char* sv = getenv("DICE_PRUNE_SURVIVORS");
-    c->prune_surv_evals = sv && *sv ? std::max(0, atoi(sv)) : kSurvMaxEvals;
     // Batches of long files go to the postings kernels whole in dice_match (top template of every
     // file): a file with more words than the largest template resembles several templates or none,
     // its bounds stay loose and it is deferred after the prune pass anyway (long/mixed files: 1.87
@@ -936,9 +728,9 @@ static int launch_prune_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s,
 // file list + count, and the postings pass's dense partials.
 int prune_reserve(dice_ctx* c, dice_batch* b) {
     int rc;
-    // two device lists of deferred files (dice_prune4's, the survivors kernel's) and their lengths
-    if (!b->d_defer && ((rc = dalloc_bytes((void**)&b->d_defer, (size_t)b->capacity * 8)) ||
-                        (rc = dalloc_bytes((void**)&b->d_ndefer, 8))))
+    // the device list of deferred files and its length
+    if (!b->d_defer && ((rc = dalloc_bytes((void**)&b->d_defer, (size_t)b->capacity * 4)) ||
+                        (rc = dalloc_bytes((void**)&b->d_ndefer, 4))))
         return rc;
     // one exact-score count per wave of each persistent grid (at most 32 waves per CU each)
     if (!b->d_nscored && (rc = dalloc_bytes((void**)&b->d_nscored, (size_t)std::max(c->n_cu, 1) * 64 * 4 + 128 * 4)))
@@ -954,56 +746,11 @@ int prune_reserve(dice_ctx* c, dice_batch* b) {
 // that matches nothing reports confidence 0, not its top score, so only templates that can reach
 // the threshold need an exact score -- the drop level starts at the threshold (keys are in units
 // of score / 400; the 2^-11 margin covers the keys' f32 evaluation as for the best score).
-template <int J, int TJ>
-static int launch_survivors(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0, bool conf) {
-    constexpr int NW = kSurvWaves;
-    const size_t tp = (size_t)TJ * kWave;
-    const size_t lds = (size_t)NW * ((J + 1) / 2) * 2 * kWave * 8 + ((tp * (32 + 16 + 4 + 4) + (tp + 1) * 4 + 15) / 16) * 16;
-    auto kern = dice_prune_survivors<J, TJ, NW>;
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return fail(DICE_E_DEVICE, "hipFuncSetAttribute failed");
-    // persistent over the device list (its length stays on the device): every resident workgroup
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / NW, (160 * 1024) / (int64_t)lds));
-    const int64_t groups = per_cu * c->n_cu;
-    Prune4Args pa;
-    pa.q8 = (const uint4*)c->d_p4q8;
-    pa.tc = (const uint4*)c->d_p4tc;
-    pa.ccm = (const uint32_t*)c->d_p4cc;
-    pa.srec = (const uint32_t*)c->d_p4off;
-    pa.qrec = (const uint4*)c->d_p4rec;
-    pa.slot = (const uint4*)c->d_p4slot;
-    for (int k = 0; k < 2; ++k) {
-        pa.zkeep[k] = c->p4_zkeep[k];
-        pa.zpos[k] = c->p4_zpos[k];
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(NW * kWave), lds, s, (const uint64_t*)b->d_rows, c->w64,
-                       c->T, pa, (const uint4*)c->d_p4q32, (const uint32_t*)c->d_p4s32, b->d_wf, b->d_len, b->d_cc, thr,
-                       b->d_best, b->d_ov, b->d_score, c->post_fast, c->prune_zero_base, b->d_defer, b->d_ndefer,
-                       b->d_defer + b->capacity, b->d_ndefer + 1, c->prune_surv_evals, llo0, conf,
-                       b->d_nscored + b->prune_waves);
-    b->surv_waves = groups * NW;
-    return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_prune_survivors launch failed");
-}
-
-template <int J>
-static int launch_survivors_j(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, float llo0, bool conf) {
-    switch (prune_tj(c->T)) {
-        case 2: return launch_survivors<J, 2>(c, b, thr, s, llo0, conf);
-        case 4: return launch_survivors<J, 4>(c, b, thr, s, llo0, conf);
-        case 6: return launch_survivors<J, 6>(c, b, thr, s, llo0, conf);
-        case 8: return launch_survivors<J, 8>(c, b, thr, s, llo0, conf);
-        case 10: return launch_survivors<J, 10>(c, b, thr, s, llo0, conf);
-        default: return launch_survivors<J, (kPruneMaxT + kWave - 1) / kWave>(c, b, thr, s, llo0, conf);
-    }
-}
-
 int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bool confidence) {
     if (b->n == 0) return DICE_OK;
     int rc;
     if ((rc = prune_reserve(c, b))) return rc;
-    // both device list lengths (dice_prune4's deferred files, the survivors kernel's) in one fill
-    if (hipMemsetAsync(b->d_ndefer, 0, 8, s) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
-    b->surv_waves = 0;
+    if (hipMemsetAsync(b->d_ndefer, 0, 4, s) != hipSuccess) return fail(DICE_E_DEVICE, "hipMemsetAsync failed");
     const float llo0 = confidence && thr > 0 ? (float)(thr / 400.0 * (1.0 - 1.0 / 2048)) : -1.0f;
     switch ((c->w64 + kWave - 1) / kWave) {
         case 1: rc = launch_prune_j<1>(c, b, thr, s, llo0, confidence); break;
@@ -1015,20 +762,6 @@ int prune_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s, bo
         default: rc = launch_prune_j<8>(c, b, thr, s, llo0, confidence); break;
     }
     if (rc) return rc;
-    if (c->prune_surv_evals > 0) {
-        // the deferred files through the 32-group bound; those it defers go to the postings kernels
-        switch ((c->w64 + kWave - 1) / kWave) {
-            case 1: rc = launch_survivors_j<1>(c, b, thr, s, llo0, confidence); break;
-            case 2: rc = launch_survivors_j<2>(c, b, thr, s, llo0, confidence); break;
-            case 3:
-            case 4: rc = launch_survivors_j<4>(c, b, thr, s, llo0, confidence); break;
-            case 5:
-            case 6: rc = launch_survivors_j<6>(c, b, thr, s, llo0, confidence); break;
-            default: rc = launch_survivors_j<8>(c, b, thr, s, llo0, confidence); break;
-        }
-        if (rc) return rc;
-        return post_launch_match_indexed(c, b, thr, b->d_defer + b->capacity, b->d_ndefer + 1, s, confidence);
-    }
     return post_launch_match_indexed(c, b, thr, b->d_defer, b->d_ndefer, s, confidence);
 }
 

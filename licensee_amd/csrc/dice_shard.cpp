@@ -162,11 +162,16 @@ bool enable_peer(dice_ctx* from, int to) {
 }
 
 // Before a device gather: peer access from every shard's device to ctxs[0]'s; records whether
-// all of them have it (dice_last_gather_peer).
+// all of them have it (dice_last_gather_peer: 1 / 0), or -1 when every ctx sits on ctxs[0]'s
+// device -- no shard crosses devices, so the call says nothing about a peer path.
 void prepare_device_gather(dice_ctx* const* ctxs, int32_t n_ctx) {
-    bool all = true;
-    for (int32_t i = 1; i < n_ctx; ++i) all = enable_peer(ctxs[i], ctxs[0]->device) && all;
-    g_last_gather_peer = all ? 1 : 0;
+    bool all = true, remote = false;
+    for (int32_t i = 1; i < n_ctx; ++i) {
+        if (ctxs[i]->device == ctxs[0]->device) continue;
+        remote = true;
+        all = enable_peer(ctxs[i], ctxs[0]->device) && all;
+    }
+    g_last_gather_peer = !remote ? -1 : all ? 1 : 0;
 }
 
 // Device gather buffer on ctxs[0]'s device: `bytes` bytes, freed by the caller.

@@ -79,8 +79,9 @@ def test_bench_abi_sharded_leg_three_contexts():
     assert rec['contexts'] == 3 and rec['devices'] == [0, 0, 0] and rec['files'] == 50000
     for mode in ('host', 'device'):
         assert rec[mode]['mismatches'] == 0 and rec[mode]['files_per_s'] > 0, rec
-    assert rec['host']['dice_last_gather_peer'] == -1 and rec['device']['dice_last_gather_peer'] in (0, 1)
-    assert rec['winner'] in ('host', 'device')
+    # one device: no peer path exercised, and no gather winner claimed from same-device timings
+    assert rec['host']['dice_last_gather_peer'] == -1 and rec['device']['dice_last_gather_peer'] == -1
+    assert rec['winner'] is None and 'distinct device' in rec['winner_reason']
 
 
 def test_config3_traffic_file_per_entry_point():

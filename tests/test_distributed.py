@@ -49,6 +49,14 @@ def _worker(rank, world, port, n_per, out_path, use_gpu):
     out = all_gather_packed(torch.from_numpy(res))
     to0 = gather_packed_to0(torch.from_numpy(res))
     assert (to0 is None) == (rank != 0)
+    # bench.py's collective gather leg (the RCCL leg of gather_compare, here over gloo with host
+    # tensors): its packing, shard order and timing reduction
+    import bench
+    group = bench.Group(rank, world, 'gloo')
+    leg_dst = torch.empty((world * n_per, 4), dtype=torch.int32) if rank == 0 else None
+    leg_s = bench.collective_gather_leg(torch.from_numpy(res), leg_dst, group, rank, 2, lambda: None)
+    assert leg_s > 0
+    assert bench.gather_winner(leg_s, leg_s) == 'host' and bench.gather_winner(2.0, 1.0) == 'rccl'
     shared = SharedResults(f'licensee_test_{port}', world, n_per, create=rank == 0) if rank == 0 else None
     dist.barrier()                       # the segment exists before the other ranks attach
     if shared is None:
@@ -62,6 +70,7 @@ def _worker(rank, world, port, n_per, out_path, use_gpu):
     if rank == 0:
         np.save(out_path, out.numpy())
         np.save(out_path + '.to0.npy', to0.numpy())
+        np.save(out_path + '.leg.npy', leg_dst.numpy())
         np.save(out_path + '.shm.npy', pack_results(shared.best.copy(), shared.overlap.copy(), shared.score.copy()))
     dist.barrier()
     shared.close()
@@ -80,6 +89,7 @@ def test_two_rank_shard_and_gather(tmp_path, use_gpu):
     mp.start_processes(_worker, args=(world, _free_port(), n_per, out_path, use_gpu), nprocs=world, start_method='spawn')
     gathered = np.load(out_path)
     assert np.array_equal(np.load(out_path + '.to0.npy'), gathered)
+    assert np.array_equal(np.load(out_path + '.leg.npy'), gathered)
     assert np.array_equal(np.load(out_path + '.shm.npy'), gathered)
     corpus = TemplateCorpus(License.all(hidden=True, pseudo=False))
     fb = SyntheticCorpus(corpus).generate(0, world * n_per, seed=7, nthreads=2)

@@ -48,13 +48,10 @@ def test_corpus_size(n_templates, kernel, monkeypatch):
     _check_corpus(n_templates, kernel, monkeypatch)
 
 
-# the postings kernels' dense-prefix variants: the matrix-core kernel (default, int8
-# and FP4 forms) with 3 or 2 32-file M-tiles per tile (12 waves, tp <= 640) and its 11-wave form
-# above 640 templates (672, 700), the VALU kernel (DICE_POST_MFMA=0), and the FP4 kernel with byte
-# partial rows for files with <= 255 prefix words (DICE_POST_U8=1, A/B)
-PREFIX_VARIANTS = {'fp4-mt3': {}, 'fp4-mt2': {'DICE_POST_MFMA_MT': '2'}, 'valu': {'DICE_POST_MFMA': '0'},
-                   'fp4-u8': {'DICE_POST_U8': '1'},
-                   'int8-mt3': {'DICE_POST_MFMA': '1'}, 'int8-mt2': {'DICE_POST_MFMA': '1', 'DICE_POST_MFMA_MT': '2'}}
+# the postings kernels' dense prefix in both launch shapes of the matrix-core kernel: 12 waves x 3
+# 32-file M-tiles up to 640 templates (130, 600) and 11 waves x 2 M-tiles above (672, 700), plus
+# narrower prefixes (DICE_POST_DENSE: 4 and 12 words)
+PREFIX_VARIANTS = {'d20': {}, 'd4': {'DICE_POST_DENSE': '4'}, 'd12': {'DICE_POST_DENSE': '12'}}
 
 
 @pytest.mark.parametrize('variant', sorted(PREFIX_VARIANTS))

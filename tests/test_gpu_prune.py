@@ -86,14 +86,8 @@ def test_config3_files(config3, monkeypatch):
     assert 0.3 < np.mean(best >= 0) < 0.9   # the workload matches some files, not all
 
 
-# (DICE_PRUNE_SURVIVORS: exact scores per deferred file in the 32-group survivors kernel before
-# the postings kernels take it; 0, the default = no survivors kernel)
 KNOBS = [{}, {'DICE_PRUNE_MAX_EVALS': '1'}, {'DICE_PRUNE_MAX_EVALS': '0'}, {'DICE_PRUNE_ROUTE': '0'},
-         {'DICE_PRUNE_ROUTE_AT': '1'}, {'DICE_PRUNE_ROUTE': '600', 'DICE_PRUNE_ROUTE_AT': '4'},
-         {'DICE_PRUNE_SURVIVORS': '32'}, {'DICE_PRUNE_MAX_EVALS': '1', 'DICE_PRUNE_SURVIVORS': '1'},
-         {'DICE_PRUNE_ROUTE': '0', 'DICE_PRUNE_SURVIVORS': '3'},
-         # the deferred files' partials as byte rows where their prefix allows (indexed positions)
-         {'DICE_PRUNE_ROUTE': '0', 'DICE_POST_U8': '1'}]
+         {'DICE_PRUNE_ROUTE_AT': '1'}, {'DICE_PRUNE_ROUTE': '600', 'DICE_PRUNE_ROUTE_AT': '4'}]
 
 
 @pytest.mark.parametrize('knob', range(len(KNOBS)))
@@ -130,14 +124,12 @@ def _random_files(c, n, seed, density):
     return FileBatch(bits, wf, ln, cc)
 
 
-@pytest.mark.parametrize('max_evals,survivors', [('8', '0'), ('0', '0'), ('1', '0'), ('1', '32'), ('8', '32'), ('1', '2')])
-def test_files_resembling_nothing(config3, max_evals, survivors, monkeypatch):
+@pytest.mark.parametrize('max_evals', ['8', '0', '1'])
+def test_files_resembling_nothing(config3, max_evals, monkeypatch):
     """Loose bounds: with deferral (DICE_PRUNE_MAX_EVALS, default 8; 1 defers every file that
-    needs a second exact score) those files are gathered and scored by the postings kernels --
-    with DICE_PRUNE_SURVIVORS=n (A/B) first bounded again with 32 word groups and scored by the
-    survivors kernel (n exact scores at most); 0 scores them all in the pruned kernel."""
+    needs a second exact score) those files are gathered and scored by the postings kernels; 0
+    scores them all in the pruned kernel."""
     monkeypatch.setenv('DICE_PRUNE_MAX_EVALS', max_evals)
-    monkeypatch.setenv('DICE_PRUNE_SURVIVORS', survivors)
     c, _ = config3
     fb = _random_files(c, 1500, seed=3, density=0.05)
     _check(c, fb, monkeypatch)
@@ -153,9 +145,8 @@ def test_dense_files(config3, monkeypatch):
                        for g in range(16)], 1)
     assert np.any(groups.max(1) > 255) and np.any(groups.max(1) <= 255)
     _check(c, fb, monkeypatch, thresholds=(98.0, 0.0))
-    # every file through the survivors kernel (deferred after one exact score): its 32 groups
-    # overflow a byte on the densest files (the coarse-bound path there too)
-    _check(c, fb, monkeypatch, thresholds=(98.0, 0.0), env={'DICE_PRUNE_MAX_EVALS': '1', 'DICE_PRUNE_SURVIVORS': '32'})
+    # every file deferred after one exact score: the postings kernels take the dense files
+    _check(c, fb, monkeypatch, thresholds=(98.0, 0.0), env={'DICE_PRUNE_MAX_EVALS': '1'})
 
 
 def test_slow_envelope_files(config3, monkeypatch):
@@ -255,6 +246,8 @@ def test_long_file_batches_route_to_postings_in_match(route, monkeypatch):
                     _assert_same(b.download_match(), exp, ('match', profile, route, thr))
                     routed = b.scored_pairs() == n * T
                     assert routed == (profile == 1 and route != '0'), (profile, route, b.scored_pairs())
+                    if routed:   # (after the previous threshold's pruned confidence call: not its stale count)
+                        assert b.deferred() == 0
                     b.match(thr, confidence=True)
                     best, ov, score = b.download_match()
                     hit = exp[0] >= 0
@@ -264,5 +257,30 @@ def test_long_file_batches_route_to_postings_in_match(route, monkeypatch):
                         assert b.scored_pairs() < n * T   # the confidence entry point stays pruned
             finally:
                 b.close()
+    finally:
+        sc.close()
+
+
+def test_empty_batch_after_pruned_call_reports_nothing(config3):
+    """An empty upload after a pruned Dice#confidence call: dice_batch_scored_pairs and
+    dice_batch_deferred report 0 for the empty batch, not the previous call's counts."""
+    from licensee_amd._native import FileBatch
+    c, fb = config3
+    sc = _scorer(c)
+    try:
+        b = sc.batch(2000)
+        try:
+            part = FileBatch(fb.bits[:2000], fb.wordset_size[:2000], fb.length[:2000], fb.cc_false_positive[:2000])
+            b.upload(part)
+            b.match(98.0, confidence=True)
+            b.download_match()
+            assert 0 < b.scored_pairs() < 2000 * len(c.templates)
+            empty = FileBatch(fb.bits[:0], fb.wordset_size[:0], fb.length[:0], fb.cc_false_positive[:0])
+            b.upload(empty)
+            for conf in (True, False):
+                b.match(98.0, confidence=conf)
+                assert b.scored_pairs() == 0 and b.deferred() == 0
+        finally:
+            b.close()
     finally:
         sc.close()

@@ -137,13 +137,17 @@ def test_sharded_rejects_duplicate_ctx(vendored):
 
 
 def test_device_gather_reports_peer_path(vendored):
-    """Shards on ctxs[0]'s own device are local (1); a host gather reports -1."""
+    """Every context on device 0 (the one-GPU box): a device gather exercises no peer path and
+    reports -1, as a host gather does; the results are those of one dice_match either way."""
     from licensee_amd._native import last_gather_peer, match_sharded
     corpus, fb, scs = vendored
-    match_sharded(scs, _sub(fb, 1000), 98.0, 1)
-    assert last_gather_peer() == 1
-    match_sharded(scs, _sub(fb, 1000), 98.0, 0)
+    assert {sc.device for sc in scs} == {0}
+    dev = match_sharded(scs, _sub(fb, 1000), 98.0, 1)
     assert last_gather_peer() == -1
+    host = match_sharded(scs, _sub(fb, 1000), 98.0, 0)
+    assert last_gather_peer() == -1
+    for a, b in zip(dev, host):
+        assert np.array_equal(a, b)
 
 
 def test_sharded_pinned_staging_large_pageable_input():

@@ -3,9 +3,8 @@
 The postings kernels and the config-3 pruned kernel are written for 8 waves per SIMD (64 VGPRs,
 two 16-wave workgroups per CU). A kernel that spills to scratch pays a reload whose vmcnt(0) waits
 for every store and load issued before it ("Matrix kernel without spills"): keep
-them at zero scratch and full occupancy. The matrix-core dense-prefix kernel holds 64 i32
-accumulators per lane (int8 form; f32 in the FP4 form) and runs at 3 waves per SIMD, also without
-scratch."""
+them at zero scratch and full occupancy. The matrix-core dense-prefix kernel holds up to 96 f32
+accumulators per lane (FP4 MFMA) and runs at 3 waves per SIMD, also without scratch."""
 import os
 import sys
 
@@ -28,10 +27,9 @@ def _resources(src):
 def test_postings_kernels_fit_8_waves_without_scratch():
     res = _resources('dice_post.hip')
     # (the matrix kernels run 8-wave workgroups at 6 waves per SIMD: three per CU)
-    # (each narrow kernel in its u16-partials and byte-row (U8) forms)
-    names = [(f'dice_post_narrow_match<{tp}, {u8}>', 8) for tp in (608, 704) for u8 in ('false', 'true')]
-    names += [(f'dice_post_narrow_matrix<1, {tp}, {u8}>', 6) for tp in (608, 704) for u8 in ('false', 'true')]
-    for name, occ in names + [('dice_post_dense<16, 608>', 8)]:
+    names = [(f'dice_post_narrow_match<{tp}>', 8) for tp in (608, 704)]
+    names += [(f'dice_post_narrow_matrix<{tp}>', 6) for tp in (608, 704)]
+    for name, occ in names:
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0', (name, r)
         assert r['VGPRs Spill'] == '0', (name, r)
@@ -46,12 +44,11 @@ def test_config3_pruned_kernel_fits_8_waves_without_scratch():
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
-def test_mfma_dense_prefix_kernel_fits_2_waves_without_scratch():
+def test_mfma_dense_prefix_kernel_fits_3_waves_without_scratch():
     res = _resources('dice_post.hip')
-    # int8 (false) and FP4 (true) forms; the FP4 kernel at the 20-word prefix the config-3 corpus uses
-    names = [f'dice_post_dense_mfma<{dp}, 2, {nw}, {mt}, {f4}, false>' for dp, f4 in ((16, 'false'), (16, 'true'), (20, 'true'))
-             for nw, mt in ((12, 2), (12, 3), (11, 2))]
-    names.append('dice_post_dense_mfma<20, 2, 12, 3, true, true>')   # byte partial rows (DICE_POST_U8=1)
+    # both launch shapes (12 waves x 3 M-tiles up to 640 templates, 11 x 2 above) at every prefix
+    # width; the config-3 corpus uses 20 words
+    names = [f'dice_post_dense_mfma<{dp}, 2, {nw}, {mt}>' for dp in (4, 8, 12, 16, 20) for nw, mt in ((12, 3), (11, 2))]
     for name in names:
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0' and r['VGPRs Spill'] == '0', (name, r)
