@@ -44,9 +44,8 @@
 namespace dice {
 
 // Phase-skip diagnostics (tools/build_variant.sh -DPOST_DIAG=n; results are wrong): 1 skips the
-// dense kernel, 2 the postings walk, 4 the narrow-word extraction, 8 scoring; 16 drops the dense
-// kernel and the partials altogether, and 16 + 32 is the fusion-cost probe (the narrow kernels then
-// do a fused prefix's matrix-core work)
+// dense kernel, 2 the postings walk, 4 the narrow-word extraction, 8 scoring. (Round 6's fusion-cost
+// probe, 16 / 48, is in the history: profiles/r6_fusion_probe.txt)
 #ifndef POST_DIAG
 #define POST_DIAG 0
 #endif
@@ -747,7 +746,7 @@ __device__ __forceinline__ void post_narrow_body(
         if ((lw & (kNarrowWaves - 1)) == (uint32_t)wave) tsc[wave][lw / kNarrowWaves] = make_uint2(twf, tlen);
     }
     // match mode: the next file's dense partials, prefetched while the wave scores the previous file
-    constexpr bool kEarly = !kMatrix && !(POST_DIAG & 16);   // (the fusion probe loads no partials)
+    constexpr bool kEarly = !kMatrix;
     uint32_t pre[kPJ];
     if (kEarly && wave < nt) load_partials<kPJ, false>(part16, f0 + wave, tp, lane, pre);
     for (int fi = wave; fi < kPostFiles; fi += kNarrowWaves) {
@@ -774,39 +773,11 @@ __device__ __forceinline__ void post_narrow_body(
             lf = (int32_t)rfl(__builtin_amdgcn_readlane(tlen, fi));
         }
         const bool cc = ((tcc >> fi) & 1u) != 0;
-        file_postings<kWCap, !kMatrix ? false : !(POST_DIAG & 16), kPJ>(row, w64, pb0, part16, pos, tpf, wq[wave], lq[wave], prow, plong, crow32,
+        file_postings<kWCap, !kEarly, kPJ>(row, w64, pb0, part16, pos, tpf, wq[wave], lq[wave], prow, plong, crow32,
                                            lanef);
         // the wave's next file's partials fly while this one is scored
         if (kEarly && fi + kNarrowWaves < nt) load_partials<kPJ, false>(part16, pos + kNarrowWaves, tpf, lane, pre);
 
-#if POST_DIAG & 32
-        // fusion-cost probe (results wrong): the per-wave share of a fused dense prefix -- 16-file
-        // rounds on v_mfma_scale_f32_16x16x128_f8f6f4, 38 N-tiles of 16 templates dealt over the
-        // 16 waves (3 each here), 10 k-steps of two prefix words: A from LDS, B from an L2-resident
-        // table (prow stands in for the masks), both widened, results ds_added into 4 rows
-        {
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            const int kb = lane >> 4, l16 = lane & 15;
-            v4f acc[3] = {};
-            const uint32_t* bsrc = reinterpret_cast<const uint32_t*>(prow);
-#pragma unroll 2
-            for (int ks = 0; ks < 10; ++ks) {
-                const v8i fa = widen_a(crow32[(ks * 4 + kb) & 255]);
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const v8i fb = widen_b(bsrc[((wave * 3 + j) * 10 + ks) * 64 + lane]);
-                    acc[j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa, fb, acc[j], 4, 4, 0, kE8M0One, 0,
-                                                                              kE8M0One);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    atomicAdd(&cnt32[(4 * kb + i) % kNarrowWaves * TPMAX + ((wave * 3 + j) * 16 + l16) % TPMAX],
-                              (uint32_t)acc[j][i]);
-        }
-#endif
         if (POST_DIAG & 8) continue;
         score_file<kMatrix, kTJ>(crow32, tcs, Tf, ldf, file, wf, lf, cc, corpus_fast, thr, best_out, ov_out, score_out,
                                  k, mov, msc, tki, tks, lanef);
@@ -1019,9 +990,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     constexpr int kNarrowWaves = narrow_waves<kMatrix>();
     const int64_t groups = idx ? std::min<int64_t>(tiles, (kNarrowWaves == 16 ? 2 : 3) * (int64_t)c->n_cu) : tiles;
     uint16_t* part16 = reinterpret_cast<uint16_t*>(b->d_pdense);
-    if (POST_DIAG & 16) {
-        // fusion probe: no dense kernel, no partials
-    } else if (c->post_dense == 0 || (POST_DIAG & 1)) {
+    if (c->post_dense == 0 || (POST_DIAG & 1)) {
         // no dense prefix: zero partials
         const size_t rows = (size_t)(idx ? b->capacity : b->n);
         if (hipMemsetAsync(part16, 0, rows * c->post_tp * 2, s) != hipSuccess)
