@@ -786,6 +786,25 @@ def main():
         t_h = time.perf_counter()
         hp.prep_files(big, None, nthreads=nthreads)
         extras['host_prep_native_files_per_s'] = len(big) / (time.perf_counter() - t_h)
+        # end to end on text: LicenseFile#license over byte strings through batch.BatchDetector's
+        # two-stage pipeline (host threads prepare batch k + 1 while batch k is on the device:
+        # upload, Exact, Dice#match + #confidence, download, Detection objects)
+        if run.cfg == 2:   # (the vendored corpus: the texts above are config-2 files)
+            from licensee_amd.batch import BatchDetector
+            from licensee_amd.dice import DiceEngine
+            det = BatchDetector(DiceEngine(device=dev), nthreads=nthreads)
+            chunks = [(big[i:i + 4000], None) for i in range(0, len(big), 4000)] * 2
+            for _ in det.detect_stream(chunks[:1]):
+                pass
+            t_h = time.perf_counter()
+            n_det = sum(len(d) for d in det.detect_stream(chunks))
+            extras['end_to_end_text_files_per_s'] = n_det / (time.perf_counter() - t_h)
+            extras['end_to_end_text_note'] = (f'batch.BatchDetector.detect_stream: {len(chunks)} batches of 4000 of '
+                                              f'the texts above, host prep ({nthreads} threads) of batch k + 1 '
+                                              f'overlapping batch k on the GPU (Copyright, Exact, Dice#match + '
+                                              f'#confidence, Detection objects)')
+            det.close()
+            det.engine.scorer.close()
         extras['host_prep_note'] = (f'normalize+intern+Copyright/Exact of synthetic texts: Python 1 thread; '
                                     f'native (csrc/normalize.cpp) {nthreads} threads on 16000 byte strings '
                                     f'(avg {sum(map(len, big)) / len(big) / 1024:.1f} KiB)')

@@ -16,7 +16,7 @@ Results equal the per-file Python chain (tests/test_gpu_golden.py::test_batch_ch
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Union
+from typing import Iterable, Iterator, List, Optional, Sequence, Tuple, Union
 
 from . import config
 from .license import License
@@ -64,22 +64,50 @@ class BatchDetector:
     def detect(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
                threshold=None) -> List[Detection]:
         thr = config.confidence_threshold() if threshold is None else threshold
+        return self._score(self._prep(contents, filenames), thr)
+
+    def detect_stream(self, batches: Iterable[Tuple[Sequence[Union[str, bytes]], Optional[Sequence[str]]]],
+                      threshold=None) -> Iterator[List[Detection]]:
+        """detect() over a stream of (contents, filenames) batches as a two-stage pipeline: the
+        native host threads prepare batch k + 1 (decode, normalize, intern, Copyright) while batch
+        k is uploaded, matched on the device and turned into Detections. Yields one list per batch,
+        in order, each equal to detect() of that batch."""
+        from concurrent.futures import ThreadPoolExecutor
+        thr = config.confidence_threshold() if threshold is None else threshold
+        it = iter(batches)
+        with ThreadPoolExecutor(1) as ex:
+            nxt = next(it, None)
+            fut = ex.submit(self._prep, *nxt) if nxt is not None else None
+            while fut is not None:
+                prepped = fut.result()
+                nxt = next(it, None)
+                fut = ex.submit(self._prep, *nxt) if nxt is not None else None
+                yield self._score(prepped, thr)
+
+    def _prep(self, contents, filenames=None):
+        """Host stage (liblicensee_host.so threads; ctypes releases the GIL during the call)."""
+        field_masks = self.exact_on == 'device'
+        fb, copyright, third, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads,
+                                                       field_masks=field_masks)
+        return fb, copyright, third
+
+    def _score(self, prepped, thr) -> List[Detection]:
+        """Device stage: Exact (device) + Dice#match/#confidence, then the matcher chain's order."""
+        fb, copyright, third = prepped
         if self.exact_on == 'device':
-            fb, copyright, fmask, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads,
-                                                           field_masks=True)
             b = self._device_batch(max(fb.n, 1))
             b.upload(fb)
-            b.exact(fmask)
+            b.exact(third)
             b.match(float(thr), confidence=True)
             exact = b.download_exact()
             best, _, score = b.download_match()
         else:
-            fb, copyright, exact, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads)
+            exact = third
             best, _, score = self.engine.scorer.match(fb, float(thr), confidence=True)
         templates = self.engine.templates
         no_license, other = License.find('no-license'), License.find('other')
         out = []
-        for i in range(len(contents)):
+        for i in range(fb.n):
             if copyright[i]:
                 out.append(Detection(no_license, 'copyright', 100))
             elif exact[i] >= 0:

@@ -260,7 +260,16 @@ def test_batch_detector_equals_per_file_chain():
               License.find('cc-by-4.0').content_normalized(), 'café licence', '', 'not a license']
     sc = SyntheticCorpus(TemplateCorpus(License.all(hidden=True, pseudo=False)))
     texts += [sc.text(i, seed=7)[0] for i in range(200)]
-    det = BatchDetector(nthreads=4).detect(texts, ['LICENSE'] * len(texts))
+    bd = BatchDetector(nthreads=4)
+    det = bd.detect(texts, ['LICENSE'] * len(texts))
+    # the two-stage pipeline (host prep of batch k + 1 beside batch k on the device): the same
+    # Detections, batch by batch, including ragged and empty batches
+    cuts = [0, 1, 64, 64, 130, len(texts)]
+    parts = [(texts[a:b], ['LICENSE'] * (b - a)) for a, b in zip(cuts, cuts[1:])]
+    streamed = [d for chunk in bd.detect_stream(parts) for d in chunk]
+    assert len(streamed) == len(det)
+    assert all((x.license.key, x.matcher, x.confidence) == (y.license.key, y.matcher, y.confidence)
+               for x, y in zip(streamed, det))
     kinds = set()
     for i, t in enumerate(texts):
         lf = LicenseFile(t, 'LICENSE')
