@@ -72,7 +72,7 @@ struct dice_ctx {
     void* d_lep = nullptr;
     void* d_les = nullptr;
     void* d_lwt = nullptr;
-    int32_t lds_nslab = 0, lds_npass = 0, lds_g = 16, lds_snake = 1, lds_wide = 0, lds_tiles = 2;
+    int32_t lds_nslab = 0, lds_npass = 0;
     int64_t lds_entries = 0;
     // kind 3 plan (dice_post.hip): postings rows of the narrow words, dense-prefix masks
     void* d_pdmt = nullptr;    // [20][kMfmaCols] u64 dense-prefix masks, word-major, zero-padded (MFMA kernel)

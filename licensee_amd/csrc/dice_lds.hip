@@ -10,14 +10,14 @@
 //   * one workgroup = 2 tiles (128 files) x 16 waves; lane l of every wave serves file l of
 //     both tiles;
 //   * the tiles' bitsets are staged through LDS in slabs of 128 u64 words per file (128 KiB),
-//     layout [pair][tile][lane] (8 B per lane: conflict-free ds_write_b64 / ds_read_b64);
+//     layout [pair][lane][tile] (a lane's words of both tiles: one 16-byte ds_read_b128);
 //   * wave w owns a contiguous template group (<= G templates per pass, balanced by record
 //     count on the host); its G x 2 accumulators stay in VGPRs for the whole pass;
 //   * one record {LDS byte offset, mask lo, mask hi, 0} per non-zero template u64 word. A
 //     wave's records for one slab are contiguous in the table (its templates are consecutive),
 //     so they stream into a per-wave 2 x 64-record LDS ring by LDS-DMA (global_load_lds_dwordx4,
 //     1 KiB per wave-instruction) and are read back with uniform-address ds_read_b128. Per
-//     step of 4 records: one ring batch, one batch of 8 ds_read_b64 file words, 16 VALU. No
+//     step of 4 records: one ring batch, one batch of 4 ds_read_b128 file words, 16 VALU. No
 //     scalar load shares the LGKM counter with the file reads (the earlier scalar-record form
 //     ran 3.5% slower: DESIGN.md section 4);
 //   * after the last pass the per-wave winners (dice_ge, later template wins exact ties) are
@@ -37,10 +37,12 @@ namespace dice {
 
 constexpr int kLdsWaves = 16;
 constexpr int kLdsBytes = 128 * 1024;                   // slab (the per-wave winners reuse it)
-// NT = tiles (files per lane) per workgroup, 2 or 4; one u64 word of every file of the
-// workgroup ("pair") is NT * 512 B, so a slab holds 128 / (NT / 2) words per file
-constexpr int pair_bytes(int nt) { return nt * kWave * 8; }
-constexpr int slab_pairs(int nt) { return kLdsBytes / pair_bytes(nt); }
+constexpr int kTiles = 2;                               // 64-file tiles per workgroup (files per lane)
+constexpr int kG = 16;                                  // templates per wave per pass
+// one u64 word of every file of the workgroup ("pair") is 2 * 512 B, so a slab holds 128 words
+// per file
+constexpr int kPairBytes = kTiles * kWave * 8;
+constexpr int kSlabPairs = kLdsBytes / kPairBytes;
 constexpr int kRing = 128;                              // records per wave ring (2 halves of 64)
 constexpr int kRingPad = 64;                            // zero records past the table end
 
@@ -65,32 +67,9 @@ __device__ __forceinline__ void ring_load4(uint32_t addr, uint4 (&c)[4]) {
         : "v"(addr));
 }
 
-// File words of 4 records (both tiles: +0 and +512 B) at precomputed LDS addresses. Plain
-// ds_read_b64 pairs: the compiler would fuse them into ds_read2st64_b64, which costs 8x.
-#define DICE_FW2(o0, o1, a) "ds_read_b64 " o0 ", " a "\n\tds_read_b64 " o1 ", " a " offset:512\n\t"
-__device__ __forceinline__ void file_load4(const uint32_t (&a)[4], uint2 (&v)[4][2]) {
-    asm volatile(
-        DICE_FW2("%0", "%1", "%8") DICE_FW2("%2", "%3", "%9") DICE_FW2("%4", "%5", "%10")
-        DICE_FW2("%6", "%7", "%11") "s_waitcnt lgkmcnt(0)"
-        : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1]),
-          "=&v"(v[3][0]), "=&v"(v[3][1])
-        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
-}
-
-// Four tiles: two ds_read_b128 per record (tiles 0-1 at +0, tiles 2-3 at +16).
-#define DICE_FW4(o0, o1, a) "ds_read_b128 " o0 ", " a "\n\tds_read_b128 " o1 ", " a " offset:16\n\t"
-__device__ __forceinline__ void file_load4w4(const uint32_t (&a)[4], uint4 (&v)[4][2]) {
-    asm volatile(
-        DICE_FW4("%0", "%1", "%8") DICE_FW4("%2", "%3", "%9") DICE_FW4("%4", "%5", "%10")
-        DICE_FW4("%6", "%7", "%11") "s_waitcnt lgkmcnt(0)"
-        : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1]),
-          "=&v"(v[3][0]), "=&v"(v[3][1])
-        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
-}
-#undef DICE_FW4
-#undef DICE_FW2
-
-// Wide layout [pair][lane][tile]: a lane's words of two tiles are one 16-byte ds_read_b128.
+// File words of 4 records at precomputed LDS addresses; the slab layout is [pair][lane][tile], so
+// a lane's words of both tiles are one 16-byte ds_read_b128 (two ds_read_b64 of a [pair][tile]
+// [lane] slab measured 1% slower, 4 tiles per workgroup 10% slower: DESIGN.md Appendix B).
 __device__ __forceinline__ void file_load4w(const uint32_t (&a)[4], uint4 (&v)[4]) {
     asm volatile(
         "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
@@ -128,17 +107,16 @@ __device__ __forceinline__ void ring_enter(int32_t p, int32_t nchunk, const uint
     }
 }
 
-template <int G, int kTiles, bool kWide>
+template <int G>
 __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
     const uint4* __restrict__ tiles, int64_t n, int32_t wq, int32_t nslab, int32_t T,
     const int32_t* __restrict__ rec, const uint4* __restrict__ ep, const int32_t* __restrict__ wave_t0,
-    int32_t npass, int32_t snake, const int4* __restrict__ tc, const uint32_t* __restrict__ wfp,
+    int32_t npass, const int4* __restrict__ tc, const uint32_t* __restrict__ wfp,
     const int32_t* __restrict__ lenp, const uint8_t* __restrict__ ccp, double thr,
     int32_t* __restrict__ best_out, uint32_t* __restrict__ ov_out, double* __restrict__ score_out) {
     // one LDS object: the rings in the low 32 KiB (LDS-DMA addresses them through M0), the
     // slab [pair][tile][lane] above them
-    constexpr int kSlabQuads = slab_pairs(kTiles) / 2;   // uint4 rows of a tile per slab
-    static_assert(kWide || kTiles == 2, "the narrow slab layout is for 2 tiles");
+    constexpr int kSlabQuads = kSlabPairs / 2;   // uint4 rows of a tile per slab
     __shared__ uint4 lds_all[kLdsWaves * kRing + kLdsBytes / 16];
     uint4 (*ring)[kRing] = reinterpret_cast<uint4 (*)[kRing]>(lds_all);
     uint2* slab = reinterpret_cast<uint2*>(lds_all + kLdsWaves * kRing);
@@ -148,27 +126,21 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
     const int64_t n_tiles = (n + kWave - 1) / kWave;
     const int64_t tile0 = (int64_t)blockIdx.x * kTiles;
 
-    // per-file |W_F|, len_F, CC flag; at 4 tiles they are re-read for every pass's epilogue
-    // (through an opaque lane index, so they are not hoisted) to keep 12 VGPRs free in the loop
-    constexpr bool kReload = kTiles == 4;
+    // per-file |W_F|, len_F, CC flag
     uint32_t my_wf[kTiles];
     int32_t my_len[kTiles];
     bool my_cc[kTiles];
     Best best[kTiles];
-    auto load_scalars = [&](int ln) {
 #pragma unroll
-        for (int f = 0; f < kTiles; ++f) {
-            const int64_t file = (tile0 + f) * kWave + ln;
-            const bool ok = file < n;
-            my_wf[f] = ok ? wfp[file] : 0;
-            my_len[f] = ok ? lenp[file] : 0;
-            my_cc[f] = ok ? ccp[file] != 0 : false;
-        }
-    };
-    if (!kReload) load_scalars(lane);
-#pragma unroll
-    for (int f = 0; f < kTiles; ++f) best[f].init();
-    const uint32_t base = lds_addr(slab) + lane * (kWide ? 8 * kTiles : 8);
+    for (int f = 0; f < kTiles; ++f) {
+        const int64_t file = (tile0 + f) * kWave + lane;
+        const bool ok = file < n;
+        my_wf[f] = ok ? wfp[file] : 0;
+        my_len[f] = ok ? lenp[file] : 0;
+        my_cc[f] = ok ? ccp[file] != 0 : false;
+        best[f].init();
+    }
+    const uint32_t base = lds_addr(slab) + lane * 8 * kTiles;
     const uint32_t ring_base = lds_addr(&ring[wave][0]);
 
     for (int pass = 0; pass < npass; ++pass) {
@@ -183,8 +155,8 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
         for (int si = 0; si < nslab; ++si) {
             // snake order: odd passes walk the slabs backwards, so a pass starts on the slab the
             // previous one ended on, which is still in LDS (npass - 1 fewer stagings)
-            const int s = (snake && (pass & 1)) ? nslab - 1 - si : si;
-            const bool restage = !(snake && pass > 0 && si == 0);
+            const int s = (pass & 1) ? nslab - 1 - si : si;
+            const bool restage = !(pass > 0 && si == 0);
             if (restage) {
                 // stage slab s: rows r = wave + 16 i of (tile f = r / 64, quad q = r % 64); one
                 // 1 KiB coalesced load per row, two ds_write_b64 per lane
@@ -202,13 +174,8 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
                 for (int i = 0; i < kTiles * kSlabQuads / kLdsWaves; ++i) {
                     const int r = wave + i * kLdsWaves;
                     const int f = r / kSlabQuads, q = r % kSlabQuads;
-                    if (kWide) {
-                        slab[((2 * q) * kWave + lane) * kTiles + f] = make_uint2(stage[i].x, stage[i].y);
-                        slab[((2 * q + 1) * kWave + lane) * kTiles + f] = make_uint2(stage[i].z, stage[i].w);
-                    } else {
-                        slab[((2 * q) * kTiles + f) * kWave + lane] = make_uint2(stage[i].x, stage[i].y);
-                        slab[((2 * q + 1) * kTiles + f) * kWave + lane] = make_uint2(stage[i].z, stage[i].w);
-                    }
+                    slab[((2 * q) * kWave + lane) * kTiles + f] = make_uint2(stage[i].x, stage[i].y);
+                    slab[((2 * q + 1) * kWave + lane) * kTiles + f] = make_uint2(stage[i].z, stage[i].w);
                 }
             }
             // this wave's record stream for slab s: runs of templates [tb, te), contiguous; the
@@ -228,52 +195,22 @@ __global__ __launch_bounds__(kLdsWaves * kWave) void dice_lds_match(
                 if (t < te) {
                     // run of (slab s, template t): a multiple of 4 records (zero-mask padding)
                     const int32_t cnt = rs[t + 1] - rs[t];
-#ifdef DICE_LDS_DIAG_NORING
-                    uint4 cr[4];
-#endif
                     for (int32_t e = 0; e < cnt; e += 4, p += 4) {
                         ring_enter(p, nchunk, src, ring[wave], lane);
                         uint4 c[4];
-#ifdef DICE_LDS_DIAG_NORING   // diagnostics only (results wrong): one ring read per run
-                        if (e == 0) ring_load4(ring_base + (uint32_t)(p & (kRing - 1)) * 16u, cr);
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) c[k] = cr[k];
-#else
                         ring_load4(ring_base + (uint32_t)(p & (kRing - 1)) * 16u, c);
-#endif
                         uint32_t fa[4];
 #pragma unroll
                         for (int k = 0; k < 4; ++k) fa[k] = base + c[k].x;
-                        if (kTiles == 4) {
-                            uint4 w[4][2];
-                            file_load4w4(fa, w);
+                        uint4 w[4];
+                        file_load4w(fa, w);
 #pragma unroll
-                            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                                for (int h = 0; h < 2; ++h)
-                                    use_record(acc[j][2 * h], acc[j][2 * h + 1], make_uint2(w[k][h].x, w[k][h].y),
-                                               make_uint2(w[k][h].z, w[k][h].w), c[k]);
-                        } else if (kWide) {
-                            uint4 w[4];
-                            file_load4w(fa, w);
-#pragma unroll
-                            for (int k = 0; k < 4; ++k)
-                                use_record(acc[j][0], acc[j][1], make_uint2(w[k].x, w[k].y), make_uint2(w[k].z, w[k].w),
-                                           c[k]);
-                        } else {
-                            uint2 v[4][2];
-                            file_load4(fa, v);
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) use_record(acc[j][0], acc[j][1], v[k][0], v[k][1], c[k]);
-                        }
+                        for (int k = 0; k < 4; ++k)
+                            use_record(acc[j][0], acc[j][1], make_uint2(w[k].x, w[k].y), make_uint2(w[k].z, w[k].w),
+                                       c[k]);
                     }
                 }
             }
-        }
-        if (kReload) {
-            int ln = lane;
-            asm volatile("" : "+v"(ln));
-            load_scalars(ln);
         }
 #pragma unroll
         for (int j = 0; j < G; ++j) {
@@ -349,19 +286,10 @@ static std::vector<int32_t> split_waves(const std::vector<int64_t>& cost, int32_
     return out;
 }
 
-// Templates per wave per pass (DICE_LDS_G): 16 measured fastest at T = 600 (24: -0.4%, 12: -2.6%;
-// tools/gpu_ab_lds.sh); 3 passes over the files there.
-static int pick_g() {
-    const char* e = getenv("DICE_LDS_G");
-    const int g = e && *e ? atoi(e) : 16;
-    return g == 12 || g == 24 ? g : 16;
-}
-
+// Templates per wave per pass: 16 measured fastest at T = 600 (24: -0.4%, 12: -2.6%); 3 passes over
+// the files there.
 int lds_setup(dice_ctx* c, const dice_templates* t) {
-    const int G = pick_g();
-    const char* ts = getenv("DICE_LDS_TILES");   // A/B knob: tiles per workgroup (2 or 4)
-    const int nt = ts && *ts == '4' ? 4 : 2;
-    const int32_t kSlabPairs = slab_pairs(nt), kPairBytes = pair_bytes(nt);
+    const int G = kG, nt = kTiles;
     const int32_t T = c->T, w64 = c->w64;
     const int32_t nslab = (w64 + kSlabPairs - 1) / kSlabPairs;
     std::vector<int32_t> rec((size_t)nslab * T + 1);
@@ -405,46 +333,17 @@ int lds_setup(dice_ctx* c, const dice_templates* t) {
     c->lds_nslab = nslab;
     c->lds_npass = npass;
     c->lds_entries = (int64_t)ep.size() - kRingPad;
-    c->lds_g = G;
-    c->lds_tiles = nt;
-    const char* sn = getenv("DICE_LDS_SNAKE");   // A/B knob: 0 = every pass walks slabs 0..nslab-1
-    c->lds_snake = !(sn && *sn == '0');
-    const char* wd = getenv("DICE_LDS_WIDE");    // A/B knob: 0 = [pair][tile][lane] slab, two ds_read_b64 per record
-    c->lds_wide = !(wd && *wd == '0');
     c->kind = 2;
     return DICE_OK;
 }
 
-template <int G, int kTiles, bool kWide>
-static void launch(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
+int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
     const int64_t n_tiles = (b->n + kWave - 1) / kWave;
     const int64_t groups = (n_tiles + kTiles - 1) / kTiles;
-    hipLaunchKernelGGL((dice_lds_match<G, kTiles, kWide>), dim3((unsigned)groups), dim3(kLdsWaves * kWave), 0, s, b->d_tiles, b->n,
+    hipLaunchKernelGGL((dice_lds_match<kG>), dim3((unsigned)groups), dim3(kLdsWaves * kWave), 0, s, b->d_tiles, b->n,
                        c->wq, c->lds_nslab, c->T, (const int32_t*)c->d_lrec, (const uint4*)c->d_lep,
-                       (const int32_t*)c->d_lwt, c->lds_npass, c->lds_snake, c->d_tc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
+                       (const int32_t*)c->d_lwt, c->lds_npass, c->d_tc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best,
                        b->d_ov, b->d_score);
-}
-
-int lds_launch_match(dice_ctx* c, dice_batch* b, double thr, hipStream_t s) {
-    if (c->lds_tiles == 4) {
-        switch (c->lds_g) {
-            case 12: launch<12, 4, true>(c, b, thr, s); break;
-            case 24: launch<24, 4, true>(c, b, thr, s); break;
-            default: launch<16, 4, true>(c, b, thr, s); break;
-        }
-    } else if (c->lds_wide) {
-        switch (c->lds_g) {
-            case 12: launch<12, 2, true>(c, b, thr, s); break;
-            case 24: launch<24, 2, true>(c, b, thr, s); break;
-            default: launch<16, 2, true>(c, b, thr, s); break;
-        }
-    } else {
-        switch (c->lds_g) {
-            case 12: launch<12, 2, false>(c, b, thr, s); break;
-            case 24: launch<24, 2, false>(c, b, thr, s); break;
-            default: launch<16, 2, false>(c, b, thr, s); break;
-        }
-    }
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_lds_match launch failed");
 }
 

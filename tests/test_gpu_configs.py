@@ -114,8 +114,7 @@ def test_config3_shard(kernel, monkeypatch):
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus
     from licensee_amd.synth_templates import synthetic_templates
-    for k in ('DICE_FORCE_DENSE', 'DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_LDS_G',
-              'DICE_POST_DENSE'):
+    for k in ('DICE_FORCE_DENSE', 'DICE_POST_DENSE'):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv('DICE_LARGE_KERNEL', 'lds' if kernel == 'lds' else 'post')
     monkeypatch.setenv('DICE_POST_PRUNE', '0' if kernel == 'post-allpairs' else '1')

@@ -95,17 +95,13 @@ def _check_corpus(n_templates, kernel, monkeypatch):
         sc.close()
 
 
-@pytest.mark.parametrize('tiles', [2, 4, 'post'])
+@pytest.mark.parametrize('kernel', ['lds', 'post'])
 @pytest.mark.parametrize('n_files', [0, 1, 63, 150, 1000])
-def test_lds_ragged_batches(n_files, tiles, monkeypatch):
-    """LDS kernel (T = 130) on batches that end mid-tile and mid-group: a workgroup holds 2 (or, as
-    the DICE_LDS_TILES=4 A/B layout, 4) tiles of 64 files, so 150 files leave a partial group and a
-    22-file tail; 0 files launch nothing. The postings kernel ('post', one 64-file tile per
-    workgroup) on the same batches."""
-    kernel = 'post' if tiles == 'post' else 'lds'
+def test_lds_ragged_batches(n_files, kernel, monkeypatch):
+    """LDS kernel (T = 130) on batches that end mid-tile and mid-group: a workgroup holds 2 tiles
+    of 64 files, so 150 files leave a partial group and a 22-file tail; 0 files launch nothing.
+    The postings kernel ('post', one 64-file tile per workgroup) on the same batches."""
     monkeypatch.setenv('DICE_LARGE_KERNEL', kernel)
-    monkeypatch.setenv('DICE_LDS_TILES', str(tiles if tiles != 'post' else 2))
-    monkeypatch.setenv('DICE_LDS_G', '12' if tiles == 4 else '16')
     from licensee_amd._native import FileBatch, Scorer
     from licensee_amd.corpus import TemplateCorpus
     from licensee_amd.synth import SyntheticCorpus

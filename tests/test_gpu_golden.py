@@ -197,14 +197,7 @@ def test_full_size_matrix_consistency(big):
     assert not np.isin(tki[flagged], cc_t).any()
 
 
-# LDS-kernel A/B layouts (dice_lds.hip): forward-only slab order, the [pair][tile][lane] slab read
-# with two ds_read_b64, and 4 tiles per workgroup (G = 12)
-LDS_VARIANTS = {'lds-fwd': {'DICE_LDS_SNAKE': '0'}, 'lds-narrow': {'DICE_LDS_WIDE': '0'},
-                'lds-t4': {'DICE_LDS_TILES': '4', 'DICE_LDS_G': '12'}}
-
-
-@pytest.mark.parametrize('kernel', ['post', 'post-d0', 'post-d4', 'post-d16', 'lds', 'lds-g12', 'lds-g24', 'lds-fwd',
-                                    'lds-narrow', 'lds-t4', 'dense'])
+@pytest.mark.parametrize('kernel', ['post', 'post-d0', 'post-d4', 'post-d16', 'lds', 'dense'])
 def test_large_corpus_600_templates(kernel, monkeypatch):
     from licensee_amd._native import Scorer
     from licensee_amd.corpus import TemplateCorpus
@@ -218,12 +211,7 @@ def test_large_corpus_600_templates(kernel, monkeypatch):
         monkeypatch.setenv('DICE_FORCE_DENSE', '1')
     else:
         monkeypatch.delenv('DICE_FORCE_DENSE', raising=False)
-    # templates per wave per pass of the LDS kernel: 16 (default, 3 passes here), 12 (4), 24 (2)
-    monkeypatch.setenv('DICE_LDS_G', kernel[5:] if kernel.startswith('lds-g') else '16')
-    for k in ('DICE_LDS_SNAKE', 'DICE_LDS_WIDE', 'DICE_LDS_TILES', 'DICE_POST_DENSE'):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in LDS_VARIANTS.get(kernel, {}).items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.delenv('DICE_POST_DENSE', raising=False)
     # postings kernel: cost-model dense prefix, or forced to 0 / 4 / 16 u64 words
     monkeypatch.setenv('DICE_LARGE_KERNEL', 'post' if kernel.startswith('post') else 'lds')
     if kernel.startswith('post-d'):
