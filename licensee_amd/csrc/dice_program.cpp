@@ -342,8 +342,7 @@ static std::string acc_block(const std::vector<Entry>& dm, size_t b, size_t e) {
 
 // Accumulations of one quad, in blocks of at most kAccBlock entries.
 static std::string acc_quad(const std::vector<Entry>& dm, size_t b0, size_t end, int32_t q) {
-    const char* be = getenv("DICE_PROG_ACC_BLOCK");   // entries per asm block (4 measured best)
-    const size_t kAccBlock = be && *be ? (size_t)std::max(1, std::min(16, atoi(be))) : 4;
+    constexpr size_t kAccBlock = 4;   // entries per asm block (2 and 8 measured slower)
     std::string out;
     const char* diag = diag_env("DICE_PROG_DIAG");   // diagnostics only: results are wrong
     if (diag && strcmp(diag, "noacc") == 0) return "acc[" + std::to_string(q) + " % NT] ^= f[0] ^ f[1] ^ f[2] ^ f[3];\n";
@@ -361,32 +360,24 @@ static void emit_macro(std::ostringstream& s, const std::string& head, const std
     s << "\n";
 }
 
-// Program order:
-//   'd' (default) dword-major: every template accumulator stays live (acc[NT]); file quads are
-//       loaded one at a time right where they are consumed, so a file dword's live range is a
-//       few instructions and the kernel runs at far lower VGPR count / higher occupancy; the
-//       epilogue (denominator, compare) runs once per template after the last quad.
-//   't' template-major: the whole file bitset is loaded up front (WQ*4 VGPRs) and each
-//       template is accumulated and retired in turn.
+// Program order: dword-major -- every template accumulator stays live (acc[NT]); file quads are
+// loaded in bursts right before they are consumed, so a file dword's live range is a few
+// instructions; the epilogue (denominator, compare) runs once per template after the last quad.
+// (The template-major order, the whole bitset loaded up front and each template retired in turn,
+// measured 2% slower and is retired: DESIGN.md Appendix B.)
 std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool corpus_fast) {
     std::ostringstream s;
     s << "#define WPB " << p.wpb << "\n";
-    const char* waves = getenv("DICE_PROG_WAVES");  // optional occupancy floor (waves/SIMD) for A/B runs
-    const char* order_env = getenv("DICE_PROG_ORDER");
-    const char order = (order_env && *order_env == 't') ? 't' : 'd';
     s << "// dice sparse program: T=" << t->n_templates << " V=" << t->n_vocab << " entries=" << p.prog.size()
-      << " order=" << order << "\n";
-    s << "#define MATCH_WAVES " << (waves && *waves ? std::string(", ") + waves : std::string()) << "\n";
+      << " order=d\n";
+    s << "#define MATCH_WAVES \n";
     uint32_t max_lf = 0;
     for (int32_t i = 0; i < t->n_templates; ++i) max_lf = std::max(max_lf, t->lf_size[i]);
-    const char* acc_asm = getenv("DICE_PROG_ACC_ASM");
-    s << "#define ACC_ASM " << ((acc_asm && *acc_asm == '0') ? 0 : 1) << "\n";
-    const char* nt = getenv("DICE_PROG_NT");
-    s << "#define FILE_NT " << ((nt && *nt == '0') ? 0 : 1) << "\n";
-    // outputs are written once and never re-read by the kernel: non-temporal stores (config 5
-    // -1.9% in A/B, 3 reps)
-    const char* nts = getenv("DICE_PROG_NTSTORE");
-    s << "#define OUT_NT " << ((nts && *nts == '0') ? 0 : 1) << "\n";
+    // v_and/v_bcnt as asm blocks (ACC_ASM; host tests compile the plain-C form), non-temporal file
+    // loads (FILE_NT) and outputs (OUT_NT: written once, never re-read; config 5 -1.9%, 3 reps)
+    s << "#define ACC_ASM 1\n";
+    s << "#define FILE_NT 1\n";
+    s << "#define OUT_NT 1\n";
     s << "#define WQ " << wq << "\n#define NT " << t->n_templates << "\n#define CORPUS_FAST "
       << (corpus_fast ? 1 : 0) << "\n#define NARROW_MUL " << (max_lf < (1u << 11) ? 1 : 0) << "\n" << kPrelude;
 
@@ -406,23 +397,7 @@ std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool
         return o.str();
     };
     std::ostringstream match_body, matrix_body, prologue;
-    if (order == 't') {
-        prologue << "u32 f[WQ * 4];\n_Pragma(\"unroll\") for (int q = 0; q < WQ; ++q) { const uint4 v = fp[q * 64]; "
-                    "f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w; }\n";
-        size_t e = 0;
-        for (int32_t i = 0; i < t->n_templates; ++i) {
-            std::ostringstream acc;
-            acc << "a = ACC_INIT(" << i << "); ";
-            for (; e < p.prog.size() && p.prog[e].tpl == i; ++e) {
-                const Entry& en = p.prog[e];
-                if (en.mask == 0xFFFFFFFFu) acc << "ACCF(" << en.dword << "); ";
-                else acc << "ACC(" << en.dword << ", 0x" << std::hex << en.mask << std::dec << "); ";
-            }
-            match_body << "{ u32 a; i32 d; " << acc.str() << den[i] << offer(i) << " }\n";
-            matrix_body << "{ u32 a; i32 d; " << acc.str() << den[i] << "MOFFER(" << i << ", "
-                        << (t->is_cc[i] ? 1 : 0) << ") }\n";
-        }
-    } else {
+    {
         std::vector<Entry> dm(p.prog);
         std::stable_sort(dm.begin(), dm.end(), [](const Entry& x, const Entry& y) {
             return x.dword != y.dword ? x.dword < y.dword : x.tpl < y.tpl;
@@ -441,47 +416,20 @@ std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool
             range.back().second = i + 1;
             cost.back() += dm[i].mask == 0xFFFFFFFFu ? 1 : 2;
         }
-        {   // processing order (DICE_PROG_QORDER): "asc" memory order; "desc" costliest quads
-            // first, so a wave's heavy accumulate work overlaps its later loads and its tail is
-            // light; "zip" (default) alternating costliest and cheapest, which spreads the VALU
+        {   // processing order: alternating costliest and cheapest quads, which spreads the VALU
             // work evenly over the stream (the packed vocabulary puts the widely shared words --
-            // 120-250 VALU per quad -- at the end, the rare ones at 4-40 first): -5.5% config 2
-            // vs memory order; "snake" equal VALU per burst
-            const char* qo = getenv("DICE_PROG_QORDER");
-            const std::string mode = qo && *qo ? qo : "zip";
+            // 120-250 VALU per quad -- at the end, the rare ones at 4-40 first): -5.5% config 2 vs
+            // memory order (costliest-first -4.4%, equal VALU per burst +-0)
             std::vector<size_t> idx(quads.size());
             for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
-            if (mode == "desc" || mode == "zip")
-                std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
-            if (mode == "zip") {
+            std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
+            {
                 std::vector<size_t> z;
                 for (size_t lo = 0, hi = idx.size(); lo < hi;) {
                     z.push_back(idx[lo++]);
                     if (lo < hi) z.push_back(idx[--hi]);
                 }
                 idx.swap(z);
-            }
-            if (mode == "snake") {   // equal VALU per burst: costliest-first dealt over bursts in snake order
-                const char* b_env2 = getenv("DICE_PROG_BURST");
-                const size_t nb2 = (size_t)std::max(1, b_env2 && *b_env2 ? atoi(b_env2) : 5);
-                const size_t ng2 = (idx.size() + nb2 - 1) / nb2;
-                std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
-                std::vector<std::vector<size_t>> bursts(ng2);
-                size_t k = 0;
-                for (size_t i = 0; i < idx.size(); ++i) {
-                    // snake over bursts that still have room
-                    for (;;) {
-                        const size_t round = k / ng2, pos = k % ng2;
-                        const size_t bi = (round % 2 == 0) ? pos : ng2 - 1 - pos;
-                        ++k;
-                        if (bursts[bi].size() < nb2) {
-                            bursts[bi].push_back(idx[i]);
-                            break;
-                        }
-                    }
-                }
-                idx.clear();
-                for (auto& b : bursts) idx.insert(idx.end(), b.begin(), b.end());
             }
             std::vector<int32_t> q2;
             std::vector<std::pair<size_t, size_t>> r2;
@@ -492,53 +440,29 @@ std::string program_source(const dice_templates* t, Program& p, int32_t wq, bool
             quads.swap(q2);
             range.swap(r2);
         }
-        // Tile layout in processing order (DICE_PROG_QLAYOUT=vocab keeps vocabulary order): tile
-        // slot i holds the vocabulary quad processed i-th (dice_pack_tiles applies p.qperm), so a
-        // wave's loads walk its 28 KiB tile front to back while the VALU work stays zipped.
+        // Tile layout in processing order: tile slot i holds the vocabulary quad processed i-th
+        // (dice_pack_tiles applies p.qperm), so a wave's loads walk its 28 KiB tile front to back
+        // while the VALU work stays zipped.
         {
-            const char* ql = getenv("DICE_PROG_QLAYOUT");
             p.qperm.clear();
-            if (!(ql && strcmp(ql, "vocab") == 0)) {
-                std::vector<char> seen((size_t)wq, 0);
-                for (int32_t q : quads) {
-                    p.qperm.push_back(q);
-                    seen[(size_t)q] = 1;
-                }
-                for (int32_t q = 0; q < wq; ++q)
-                    if (!seen[(size_t)q]) p.qperm.push_back(q);   // quads no template reads (never loaded)
-                for (size_t i = 0; i < quads.size(); ++i) quads[i] = (int32_t)i;
+            std::vector<char> seen((size_t)wq, 0);
+            for (int32_t q : quads) {
+                p.qperm.push_back(q);
+                seen[(size_t)q] = 1;
             }
+            for (int32_t q = 0; q < wq; ++q)
+                if (!seen[(size_t)q]) p.qperm.push_back(q);   // quads no template reads (never loaded)
+            for (size_t i = 0; i < quads.size(); ++i) quads[i] = (int32_t)i;
             s << "// QPERM";
             for (int32_t q : p.qperm) s << " " << q;
             s << "\n";
         }
-        const char* sched_env = getenv("DICE_PROG_SCHED");
-        const bool ring = sched_env && strcmp(sched_env, "ring") == 0;
-        if (ring) {
-            // ring of `pd` registers: quad i+pd is requested as quad i is consumed
-            const char* pd_env = getenv("DICE_PROG_PREFETCH");
-            int pd = pd_env && *pd_env ? atoi(pd_env) : 8;
-            pd = std::max(1, std::min<int>(pd, (int)quads.size()));
-            for (int i = 0; i < pd; ++i) prologue << "uint4 pf" << i << " = ldq(fp + " << quads[i] * 64 << ");\n";
-            prologue << "__builtin_amdgcn_sched_barrier(0);\n";
-            for (size_t qi = 0; qi < quads.size(); ++qi) {
-                const int slot = (int)(qi % pd);
-                prologue << "{ const uint4 v = pf" << slot << ";";
-                if (qi + pd < quads.size())
-                    prologue << " pf" << slot << " = ldq(fp + " << quads[qi + pd] * 64 << "); __builtin_amdgcn_sched_barrier(0);";
-                prologue << " const u32 f[4] = {v.x, v.y, v.z, v.w};\n";
-                prologue << acc_quad(dm, range[qi].first, range[qi].second, quads[qi]);
-                prologue << "}\n";
-            }
-        } else {
-            // bursts (default): quads in groups of `nb`, double-buffered in register sets
-            // p0_* / p1_*; group g+1 is requested (nb contiguous 1 KiB wave loads back to back)
-            // before group g is consumed. With non-temporal loads, bursts of 3 measured ~1.5% ahead
-            // of the 8-deep ring at 92 instead of 124 VGPRs, bursts of 4 (96 VGPRs) with 4-entry asm
-            // blocks another ~3.5% (same box, interleaved A/B runs, tools/gpu_ab_prog.sh).
-            const char* b_env = getenv("DICE_PROG_BURST");
-            int nb = b_env && *b_env ? atoi(b_env) : 5;
-            nb = std::max(1, std::min<int>(nb, (int)quads.size()));
+        {
+            // bursts: quads in groups of `nb` = 5, double-buffered in register sets p0_* / p1_*;
+            // group g+1 is requested (nb contiguous 1 KiB wave loads back to back) before group g
+            // is consumed. With non-temporal loads, bursts of 3 measured ~1.5% ahead of an 8-deep
+            // ring at 92 instead of 124 VGPRs, 4 another ~3.5%, 5 another 1.8% (6: -0.3%)
+            const int nb = std::max(1, std::min<int>(5, (int)quads.size()));
             const size_t ng = (quads.size() + nb - 1) / nb;
             auto group_loads = [&](std::ostringstream& o, size_t g, int set) {
                 for (size_t i = g * nb; i < std::min(quads.size(), (g + 1) * nb); ++i)
@@ -654,8 +578,7 @@ static bool corpus_in_fast_envelope(const dice_templates* t) {
 static std::string source_for(const dice_templates* t, Program& prog) {
     const int32_t w64 = (t->n_vocab + 63) / 64;
     build_entries(t, w64, prog);
-    const char* wpb = getenv("DICE_PROG_WPB");   // waves per workgroup (A/B runs; default 4)
-    prog.wpb = wpb && *wpb ? std::max(1, std::min(16, atoi(wpb))) : 4;
+    prog.wpb = 4;   // waves per workgroup (1, 2 and 8 within +-1.5%)
     return program_source(t, prog, (w64 + 1) / 2, corpus_in_fast_envelope(t));
 }
 
