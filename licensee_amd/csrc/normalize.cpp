@@ -34,6 +34,7 @@
 
 using rx::Regex;
 using rx::Str;
+using rx::Str8;
 
 // Per-pass timing (diagnostic builds only: -DLH_PASS_TIMING, tools/host_prep_passes.py). PASS
 // wraps one step of the pipeline and adds its wall time to a per-thread table.
@@ -97,45 +98,44 @@ inline uint32_t spell_tok_slot(char32_t first, char32_t last, size_t len) {
 
 bool is_strip_char(char32_t c) { return c == 0 || c == ' ' || (c >= '\t' && c <= '\r'); }
 
-Str ruby_strip(const Str& s) {
+// Texts are normalized as UTF-32 (Str) or, when every character is ASCII, as bytes (Str8: the
+// same passes over a quarter of the memory). cp: a text character as a code point; LIT: a
+// literal in the text's character type.
+inline char32_t cp(char32_t c) { return c; }
+inline char32_t cp(char c) { return (unsigned char)c; }
+template <class C>
+constexpr const C* lit_of(const char* a, const char32_t* u) {
+    if constexpr (sizeof(C) == 1) return a;
+    else return u;
+}
+#define LIT(x) lit_of<C>(x, U##x)
+
+template <class S>
+S ruby_strip(const S& s) {
     size_t a = 0, b = s.size();
-    while (a < b && is_strip_char(s[a])) ++a;
-    while (b > a && is_strip_char(s[b - 1])) --b;
+    while (a < b && is_strip_char(cp(s[a]))) ++a;
+    while (b > a && is_strip_char(cp(s[b - 1]))) --b;
     return s.substr(a, b - a);
 }
 
-// Literal search over code points: a vector scan for positions holding the literal's first
-// and last characters, then a compare at each candidate (std::u32string::find steps one
-// character at a time).
-size_t find_lit(const Str& s, const char32_t* lit, size_t from = 0) {
-    size_t m = 0;
-    while (lit[m]) ++m;
-    const size_t n = s.size();
-    if (m == 0) return from <= n ? from : Str::npos;
-    if (n < m) return Str::npos;
-    const char32_t* p = s.data();
-    const char32_t c0 = lit[0], c1 = lit[m - 1];
+// Literal search: a vector scan for positions holding the literal's first and last characters,
+// then a compare at each candidate (basic_string::find steps one character at a time).
+template <class C>
+size_t find_lit(const std::basic_string<C>& s, const C* lit, size_t from = 0) {
+    const size_t m = std::char_traits<C>::length(lit), n = s.size();
+    if (m == 0) return from <= n ? from : std::basic_string<C>::npos;
+    if (n < m || from > n - m) return std::basic_string<C>::npos;
+    const C* p = s.data();
+    const char32_t c0 = cp(lit[0]), c1 = cp(lit[m - 1]);
     const size_t last = n - m;   // last candidate start
-    size_t i = from;
-#if defined(__AVX2__)
-    const __m256i v0 = _mm256_set1_epi32((int)c0), v1 = _mm256_set1_epi32((int)c1);
-    for (; i + 8 <= last + 1; i += 8) {
-        const __m256i a = _mm256_cmpeq_epi32(_mm256_loadu_si256((const __m256i*)(p + i)), v0);
-        const __m256i b = _mm256_cmpeq_epi32(_mm256_loadu_si256((const __m256i*)(p + i + m - 1)), v1);
-        uint32_t mask = (uint32_t)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_and_si256(a, b)));
-        while (mask) {
-            const size_t j = i + (size_t)__builtin_ctz(mask);
-            if (std::char_traits<char32_t>::compare(p + j, lit, m) == 0) return j;
-            mask &= mask - 1;
-        }
-    }
-#endif
-    for (; i <= last; ++i)
-        if (p[i] == c0 && std::char_traits<char32_t>::compare(p + i, lit, m) == 0) return i;
-    return Str::npos;
+    for (size_t i = scan::find_pair(p, from, last, m - 1, c0, c0, c1, c1); i <= last;
+         i = scan::find_pair(p, i + 1, last, m - 1, c0, c0, c1, c1))
+        if (std::char_traits<C>::compare(p + i, lit, m) == 0) return i;
+    return std::basic_string<C>::npos;
 }
 
-bool contains(const Str& s, const char32_t* lit) { return find_lit(s, lit) != Str::npos; }
+template <class C>
+bool contains(const std::basic_string<C>& s, const C* lit) { return find_lit(s, lit) != std::basic_string<C>::npos; }
 
 // non-ASCII code points whose Python semantics match the ASCII rules used here: no case
 // mapping, not \w (str.isalnum() is False) -- punctuation, symbols, spaces, BOM.
@@ -232,9 +232,31 @@ inline WordKey word_key(const std::string& w) {
     return k;
 }
 
-inline bool tail_equal(const std::string& w, const char32_t* p) {
+// key of the ASCII bytes p[0, n) (the byte path; the same key as the code points')
+inline WordKey word_key(const char* p, size_t n, size_t room) {
+    WordKey k;
+    k.len = (uint32_t)n;
+    const size_t m = n < 16 ? n : 16;
+    if (room >= 16) {
+        memcpy(&k.lo, p, 8);
+        memcpy(&k.hi, p + 8, 8);
+        k.lo &= kByteMasks.lo[m];
+        k.hi &= kByteMasks.hi[m];
+    } else {
+        for (size_t i = 0; i < m; ++i) {
+            const uint64_t b = (unsigned char)p[i];
+            if (i < 8) k.lo |= b << (8 * i);
+            else k.hi |= b << (8 * (i - 8));
+        }
+    }
+    k.h = key_mix(k.lo, k.hi, n, n > 16 ? tail_hash((const unsigned char*)p, n) : 0);
+    return k;
+}
+
+template <class C>
+inline bool tail_equal(const std::string& w, const C* p) {
     for (size_t i = 16; i < w.size(); ++i)
-        if ((char32_t)(unsigned char)w[i] != p[i]) return false;
+        if ((char32_t)(unsigned char)w[i] != cp(p[i])) return false;
     return true;
 }
 
@@ -283,7 +305,8 @@ struct VocabTable {
             }
         }
     }
-    int32_t find(const WordKey& k, const char32_t* p) const {
+    template <class C>
+    int32_t find(const WordKey& k, const C* p) const {
         if (key.empty()) return -1;
         const uint32_t t = tag(k.h);
         for (size_t b = k.h & bmask;; b = (b + 1) & bmask) {
@@ -325,8 +348,12 @@ struct WordSet {
     std::vector<Slot> slot;
     uint32_t cur = 0;
     size_t count = 0, mask = 0;
-    const Str* text = nullptr;
-    void reset(const Str& s) {
+    const char32_t* t32 = nullptr;   // the file's text (one of the two)
+    const char* t8 = nullptr;
+    template <class C>
+    void reset(const C* text) {
+        if constexpr (sizeof(C) == 1) t8 = text, t32 = nullptr;
+        else t32 = text, t8 = nullptr;
         if (slot.empty()) slot.assign(1024, Slot{0, 0, 0, 0, 0, 0});
         mask = slot.size() - 1;
         if (++cur == 0) {   // epoch wrapped: clear once
@@ -334,7 +361,6 @@ struct WordSet {
             cur = 1;
         }
         count = 0;
-        text = &s;
     }
     void grow() {
         std::vector<Slot> old;
@@ -349,7 +375,8 @@ struct WordSet {
         }
     }
     // true when the token [a, a + k.len) is a new word
-    bool insert(size_t a, const WordKey& k) {
+    template <class C>
+    bool insert(const C* text, size_t a, const WordKey& k) {
         for (size_t j = k.h & mask;; j = (j + 1) & mask) {
             Slot& s = slot[j];
             if (s.epoch != cur) {
@@ -358,7 +385,7 @@ struct WordSet {
                 return true;
             }
             if (s.lo == k.lo && s.hi == k.hi && s.len == k.len &&
-                (k.len <= 16 || text->compare(s.start, k.len, *text, a, k.len) == 0))
+                (k.len <= 16 || std::char_traits<C>::compare(text + s.start, text + a, k.len) == 0))
                 return false;
         }
     }
@@ -367,7 +394,8 @@ struct WordSet {
         for (size_t j = k.h & mask;; j = (j + 1) & mask) {
             const Slot& s = slot[j];
             if (s.epoch != cur) return false;
-            if (s.lo == k.lo && s.hi == k.hi && s.len == k.len && (k.len <= 16 || tail_equal(w, text->data() + s.start)))
+            if (s.lo == k.lo && s.hi == k.hi && s.len == k.len &&
+                (k.len <= 16 || (t8 ? tail_equal(w, t8 + s.start) : tail_equal(w, t32 + s.start))))
                 return true;
         }
     }
@@ -376,6 +404,8 @@ struct WordSet {
 struct Ctx {
     std::map<std::string, Regex> re;
     std::vector<std::pair<Str, Str>> spell;
+    std::vector<Str8> spell_to8;   // the replacements as bytes (byte path; all ASCII when ascii_path)
+    bool ascii_path = true;        // ASCII texts take the byte path
     // spelling keys as a trie over a small alphabet (spell_sym: ASCII -> 1..kSpellSyms-1, 0 = not
     // in any key); node 0 is the root, child 0 = none; spell_key: key index ending at a node
     uint8_t spell_sym[128] = {};
@@ -402,14 +432,16 @@ struct Ctx {
     const Regex& R(const char* name) const { return re.at(name); }
 };
 
+template <class S>
 struct Normalizer {
+    using C = typename S::value_type;
     const Ctx& c;
-    Str cur;
+    S cur;
     bool clean = false;   // cur is already squeezed and stripped (a strip op without a match is a no-op)
 
     // squeeze(' ').strip in place (String#squeeze / #strip: only ' ' runs, \0\t\n\v\f\r ends)
     void squeeze_strip() {
-        char32_t* p = cur.data();
+        C* p = cur.data();
         const size_t n = cur.size();
         const size_t r = scan::find_double_space(p, 0, n);   // nothing to squeeze before it
         if (r < n) cur.resize(scan::squeeze_runs(p, r, r, n, true, false));
@@ -417,20 +449,20 @@ struct Normalizer {
     }
     void strip_ends() {
         size_t b = cur.size();
-        while (b > 0 && is_strip_char(cur[b - 1])) --b;
+        while (b > 0 && is_strip_char(cp(cur[b - 1]))) --b;
         cur.resize(b);
         size_t a = 0;
-        while (a < cur.size() && is_strip_char(cur[a])) ++a;
+        while (a < cur.size() && is_strip_char(cp(cur[a]))) ++a;
         if (a) cur.erase(0, a);
     }
     // strip(re): gsub(re, ' ').squeeze(' ').strip (content_helper.rb:223-236)
     void strip_re(const Regex& r) {
-        if (!r.sub_into(cur, U" ") && clean) return;
+        if (!r.sub_into(cur, S(LIT(" "))) && clean) return;
         squeeze_strip();
         clean = true;
     }
-    void sub_re(const Regex& r, const char32_t* repl) {
-        if (r.sub_into(cur, Str(repl))) clean = false;
+    void sub_re(const Regex& r, const C* repl) {
+        if (r.sub_into(cur, S(repl))) clean = false;
     }
 
     void strip_title() {
@@ -446,12 +478,12 @@ struct Normalizer {
     // strip_comments (content_helper.rb:263-267): when every line of String#split("\n") (trailing
     // empty fields dropped) matches comment_markup ^[ \t\n\v\f\r]*?[/*]{1,2} -- on a line: its
     // first character outside [ \t\v\f\r] is '/' or '*' -- and there is not exactly one line
-    static bool comment_line(const char32_t* p, size_t a, size_t b) {
+    static bool comment_line(const C* p, size_t a, size_t b) {
         while (a < b && (p[a] == ' ' || p[a] == '\t' || p[a] == '\v' || p[a] == '\f' || p[a] == '\r')) ++a;
         return a < b && (p[a] == '/' || p[a] == '*');
     }
     void strip_comments() {
-        const char32_t* p = cur.data();
+        const C* p = cur.data();
         size_t end = cur.size();
         while (end > 0 && p[end - 1] == '\n') --end;   // trailing empty fields
         if (end > 0 && scan::find_char(p, 0, end, U'\n') == end) return;   // one line
@@ -464,7 +496,7 @@ struct Normalizer {
     }
 
     // hyphenated (content_helper.rb:40) can only match a '-' followed by [ \t\v\f\r]* and '\n'
-    static bool has_hyphen_break(const Str& s) {
+    static bool has_hyphen_break(const S& s) {
         for (size_t i = scan::find_char(s.data(), 0, s.size(), U'-'); i < s.size();
              i = scan::find_char(s.data(), i + 1, s.size(), U'-')) {
             size_t j = i + 1;
@@ -479,7 +511,7 @@ struct Normalizer {
     // path has ASCII word characters only, so \b is the ASCII boundary.
     void spelling() {
         const size_t n = cur.size();
-        const char32_t* p = cur.data();
+        const C* p = cur.data();
         auto word = [](char32_t ch) {   // Python \b's \w
             return ch < 128 ? kAsciiWord[ch] != 0 : rx::is_word_char(ch);
         };
@@ -488,13 +520,13 @@ struct Normalizer {
         auto match_at = [&](size_t i, size_t& klen) -> int {
             int node = 0, best = -1;
             for (size_t j = i; j < n; ++j) {
-                const char32_t cj = p[j];
+                const char32_t cj = cp(p[j]);
                 const int sym = cj < 128 ? c.spell_sym[cj] : 0;
                 if (!sym) break;
                 node = c.spell_trie[(size_t)node * kSpellSyms + sym];
                 if (node <= 0) break;
                 const int ki = c.spell_key[node];
-                if (ki >= 0 && (best < 0 || ki < best) && (j + 1 == n || !word(p[j + 1]))) {
+                if (ki >= 0 && (best < 0 || ki < best) && (j + 1 == n || !word(cp(p[j + 1])))) {
                     best = ki;
                     klen = j + 1 - i;
                 }
@@ -505,7 +537,7 @@ struct Normalizer {
         // \w run starting there equals the key's first \w run (keys end in a letter, and \b
         // follows). Word starts come from 64-character \w masks; a start is tried only when
         // its run's (first, last, length) is that of some key's first run (spell_tok).
-        Str out;
+        S out;
         size_t copied = 0;   // cur[0, copied) is in out (or there is no match yet)
         uint64_t prev_word = 0;
         for (size_t b0 = 0; b0 < n; b0 += 64) {
@@ -515,7 +547,7 @@ struct Normalizer {
             while (hi) {
                 const int j = __builtin_ctzll(hi);
                 hi &= hi - 1;
-                if (rx::is_word_char(p[b0 + (size_t)j])) w |= 1ull << j;
+                if (rx::is_word_char(cp(p[b0 + (size_t)j]))) w |= 1ull << j;
             }
             uint64_t starts = w & ~((w << 1) | prev_word);
             prev_word = w >> 63;
@@ -531,20 +563,21 @@ struct Normalizer {
                     if (s0 + len > n) len = n - s0;
                 } else {
                     len = 64 - off;
-                    while (s0 + len < n && word(p[s0 + len])) ++len;
+                    while (s0 + len < n && word(cp(p[s0 + len]))) ++len;
                 }
-                if (!spell_tok_hit(p[s0], p[s0 + len - 1], len)) continue;
+                if (!spell_tok_hit(cp(p[s0]), cp(p[s0 + len - 1]), len)) continue;
                 size_t klen = 0;
                 const int key = match_at(s0, klen);
                 if (key < 0) continue;
                 if (out.empty() && copied == 0) out.reserve(n + 16);
                 out.append(cur, copied, s0 - copied);
-                out += c.spell[(size_t)key].second;
+                if constexpr (sizeof(C) == 1) out += c.spell_to8[(size_t)key];
+                else out += c.spell[(size_t)key].second;
                 copied = s0 + klen;
             }
         }
         if (copied == 0 && out.empty()) return;   // no varietal word: nothing to rebuild
-        out.append(cur, copied, Str::npos);
+        out.append(cur, copied, S::npos);
         cur.swap(out);
         clean = false;
     }
@@ -560,6 +593,23 @@ struct Normalizer {
     void downcase_quote_ascii(size_t& amps) {
         size_t i = 0;
 #if defined(__AVX2__)
+        if constexpr (sizeof(C) == 1) {   // the byte path: every block is ASCII
+            char* p = cur.data();
+            const size_t n = cur.size();
+            const __m256i A1 = _mm256_set1_epi8('A' - 1), Z1 = _mm256_set1_epi8('Z' + 1), c32 = _mm256_set1_epi8(32);
+            const __m256i dq = _mm256_set1_epi8('"'), bt = _mm256_set1_epi8('`'), sq = _mm256_set1_epi8('\'');
+            const __m256i amp = _mm256_set1_epi8('&');
+            for (; i + 32 <= n; i += 32) {
+                __m256i v = _mm256_loadu_si256((const __m256i*)(p + i));
+                const __m256i up = _mm256_and_si256(_mm256_cmpgt_epi8(v, A1), _mm256_cmpgt_epi8(Z1, v));
+                v = _mm256_add_epi8(v, _mm256_and_si256(up, c32));
+                v = _mm256_blendv_epi8(v, sq, _mm256_or_si256(_mm256_cmpeq_epi8(v, dq), _mm256_cmpeq_epi8(v, bt)));
+                amps += (size_t)__builtin_popcount(scan::bytes(_mm256_cmpeq_epi8(v, amp)));
+                _mm256_storeu_si256((__m256i*)(p + i), v);
+            }
+            ascii_done_ = i;
+            return;
+        } else {
         char32_t* p = cur.data();
         const size_t n = cur.size();
         const __m256i A1 = _mm256_set1_epi32('A' - 1), Z1 = _mm256_set1_epi32('Z' + 1), c32 = _mm256_set1_epi32(32);
@@ -574,6 +624,7 @@ struct Normalizer {
             amps += (size_t)__builtin_popcount(scan::lanes(_mm256_cmpeq_epi32(v, amp)));
             _mm256_storeu_si256((__m256i*)(p + i), v);
         }
+        }
 #endif
         (void)amps;
         ascii_done_ = i;
@@ -587,13 +638,13 @@ struct Normalizer {
     }
 
     // content_without_title_and_version + content_normalized (content_helper.rb:144-168)
-    Str run(const Str& content) {
+    S run(const S& content) {
         PASS("strip", cur = ruby_strip(content));
         PASS("hrs", strip_re(c.R("hrs")));
         PASS("comments", strip_comments());
         PASS("markdown_headings", strip_re(c.R("markdown_headings")));
         // \[(.+?)\]\(.+?\) needs a literal "](": without one the lazy scans from every '[' are wasted
-        PASS("link_markup", if (contains(cur, U"](")) sub_re(c.R("link_markup"), U"\\1"));
+        PASS("link_markup", if (contains(cur, LIT("]("))) sub_re(c.R("link_markup"), LIT("\\1")));
         PASS("title", strip_title());
         PASS("version", strip_re(c.R("version")));
         // downcase, then (moved ahead of lists/https, with which they commute: neither pattern
@@ -603,42 +654,44 @@ struct Normalizer {
             size_t amps = 0;
             downcase_quote_ascii(amps);
             for (size_t i = ascii_done_; i < cur.size(); ++i) {
-                char32_t& ch = cur[i];
-                if (ch < 128) {
+                C& ch = cur[i];
+                if (cp(ch) < 128) {
                     if (ch >= 'A' && ch <= 'Z') ch += 32;
                     else if (ch == '"' || ch == '`') ch = '\'';
                     else if (ch == '&') ++amps;
-                } else if (ch == 0x2018 || ch == 0x2019 || ch == 0x201C || ch == 0x201D) {
-                    ch = '\'';
-                } else if (c.unicode) {
-                    auto it = c.lower.find(ch);
-                    if (it != c.lower.end()) ch = it->second;
+                } else if constexpr (sizeof(C) == 4) {
+                    if (ch == 0x2018 || ch == 0x2019 || ch == 0x201C || ch == 0x201D) {
+                        ch = '\'';
+                    } else if (c.unicode) {
+                        auto it = c.lower.find(ch);
+                        if (it != c.lower.end()) ch = it->second;
+                    }
                 }
             }
             if (amps) {
-                Str out;
+                S out;
                 out.reserve(cur.size() + 2 * amps);
-                for (char32_t ch : cur) {
-                    if (ch == '&') out += U"and";
+                for (C ch : cur) {
+                    if (ch == '&') out += LIT("and");
                     else out.push_back(ch);
                 }
                 cur.swap(out);
             }
             clean = false;
         });
-        PASS("lists", sub_re(c.R("lists"), U"- \\1"));
+        PASS("lists", sub_re(c.R("lists"), LIT("- \\1")));
         // the literal 'http:' (content_helper.rb:35) without the regex engine
         PASS("https", {
-            size_t at = find_lit(cur, U"http:");
-            if (at != Str::npos) {
-                Str out;
+            size_t at = find_lit(cur, LIT("http:"));
+            if (at != S::npos) {
+                S out;
                 size_t i = 0;
-                for (; at != Str::npos; at = find_lit(cur, U"http:", i)) {
+                for (; at != S::npos; at = find_lit(cur, LIT("http:"), i)) {
                     out.append(cur, i, at - i);
-                    out += U"https:";
+                    out += LIT("https:");
                     i = at + 5;
                 }
-                out.append(cur, i, Str::npos);
+                out.append(cur, i, S::npos);
                 cur.swap(out);
                 clean = false;
             }
@@ -647,27 +700,27 @@ struct Normalizer {
         // two hyphens: skip the regex when the text has neither
         PASS("dashes", {
             static const char32_t kDash[2] = {0x2014, 0x2013};
-            if (scan::find_any(cur.data(), 0, cur.size(), kDash, 2) < cur.size() || contains(cur, U"--"))
-                sub_re(c.R("dashes"), U"-");
+            if (scan::find_any(cur.data(), 0, cur.size(), kDash, 2) < cur.size() || contains(cur, LIT("--")))
+                sub_re(c.R("dashes"), LIT("-"));
         });
-        PASS("hyphenated", if (has_hyphen_break(cur)) sub_re(c.R("hyphenated"), U"\\1-\\2"));
+        PASS("hyphenated", if (has_hyphen_break(cur)) sub_re(c.R("hyphenated"), LIT("\\1-\\2")));
         PASS("spelling", spelling());
-        PASS("span_markup", sub_re(c.R("span_markup"), U"\\1"));
-        PASS("bullet", sub_re(c.R("bullet"), U"\n\n- "));
-        PASS("bullet_paren", sub_re(c.R("bullet_paren"), U")("));
+        PASS("span_markup", sub_re(c.R("span_markup"), LIT("\\1")));
+        PASS("bullet", sub_re(c.R("bullet"), LIT("\n\n- ")));
+        PASS("bullet_paren", sub_re(c.R("bullet_paren"), LIT(")(")));
         // STRIP_METHODS (content_helper.rb:89-105)
         PASS("bom", strip_re(c.R("bom")));
-        PASS("cc_optional", if (contains(cur, U"creative commons")) {
+        PASS("cc_optional", if (contains(cur, LIT("creative commons"))) {
             strip_re(c.R("cc_dedication"));
             strip_re(c.R("cc_wiki"));
         });
-        PASS("cc0_optional", if (contains(cur, U"associating cc0")) {
+        PASS("cc0_optional", if (contains(cur, LIT("associating cc0"))) {
             strip_re(c.R("cc_legal_code"));
             strip_re(c.R("cc0_info"));
             strip_re(c.R("cc0_disclaimer"));
         });
-        PASS("unlicense_optional", if (contains(cur, U"unlicense")) strip_re(c.R("unlicense_info")));
-        PASS("borders", sub_re(c.R("border_markup"), U"\\1"));
+        PASS("unlicense_optional", if (contains(cur, LIT("unlicense"))) strip_re(c.R("unlicense_info")));
+        PASS("borders", sub_re(c.R("border_markup"), LIT("\\1")));
         PASS("title2", strip_title());
         PASS("version2", strip_re(c.R("version")));
         PASS("url", strip_re(c.R("url")));
@@ -688,15 +741,18 @@ struct Normalizer {
     }
 };
 
+#undef LIT
+
 // wordset scan (content_helper.rb:109): (?:[\w/-](?:'s|(?<=s)')?)+ with ASCII \w
 inline bool wchar(char32_t c) {
     return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_' || c == '/' || c == '-';
 }
 
 // The regex's own loop from a token start: returns the token's end
-inline size_t word_end(const char32_t* s, size_t i, size_t n) {
-    while (i < n && wchar(s[i])) {
-        const char32_t ch = s[i++];
+template <class C>
+inline size_t word_end(const C* s, size_t i, size_t n) {
+    while (i < n && wchar(cp(s[i]))) {
+        const C ch = s[i++];
         if (i < n && s[i] == '\'') {
             if (i + 1 < n && s[i + 1] == 's') i += 2;
             else if (ch == 's') i += 1;
@@ -708,10 +764,8 @@ inline size_t word_end(const char32_t* s, size_t i, size_t n) {
 // Tokens are the runs of [\w/-] (64-character masks), except that a run followed by '\'' is
 // re-scanned by the regex's loop ('s and s' continue a token; an apostrophe never starts one).
 // A token ends at a character outside [\w/-], so the next one starts at a run start.
-template <class F>
-void scan_words(const Str& s, F&& emit) {
-    const char32_t* p = s.data();
-    const size_t n = s.size();
+template <class C, class F>
+void scan_words(const C* p, size_t n, F&& emit) {
     size_t resume = 0;   // end of the last token
     uint64_t prev = 0;
     for (size_t b0 = 0; b0 < n; b0 += 64) {
@@ -730,7 +784,7 @@ void scan_words(const Str& s, F&& emit) {
                 e = std::min(n, a + (size_t)__builtin_ctzll(rest));
             } else {
                 e = b0 + 64;
-                while (e < n && wchar(p[e])) ++e;
+                while (e < n && wchar(cp(p[e]))) ++e;
             }
             if (e < n && p[e] == '\'') e = word_end(p, a, n);
             emit(a, e);
@@ -756,7 +810,9 @@ bool extname_is_html(const char* fn) {
 
 struct FileOut {
     int status = 0;      // 0 ok, 1 needs the Python path, 2 error
+    bool ascii = false;  // the byte path ran: the text is normalized8
     Str normalized;
+    Str8 normalized8;
     bool cc = false, copyright = false;
 };
 
@@ -805,7 +861,53 @@ void run_workers(int32_t nthreads, F& work) {
     for (auto& id : th) pthread_join(id, nullptr);
 }
 
+// true when every byte of data[0, len) is ASCII
+bool all_ascii(const char* data, size_t len) {
+    size_t i = 0;
+#if defined(__AVX2__)
+    __m256i acc = _mm256_setzero_si256();
+    for (; i + 32 <= len; i += 32) acc = _mm256_or_si256(acc, _mm256_loadu_si256((const __m256i*)(data + i)));
+    if (_mm256_movemask_epi8(acc)) return false;
+#endif
+    for (; i < len; ++i)
+        if ((unsigned char)data[i] >= 0x80) return false;
+    return true;
+}
+
+// the byte path of prep_one_impl: an ASCII text (every character's Python semantics is the
+// ASCII rule; decoding is the identity)
+void prep_ascii(const Ctx& c, const char* data, int64_t len, bool is_file, FileOut& o) {
+    Str8 content;
+    if (is_file) {   // universal newline (project_file.rb:41)
+        content.resize((size_t)len);
+        size_t w = 0;
+        for (size_t i = 0; i < (size_t)len; ++i) {
+            if (data[i] == '\r') {
+                content[w++] = '\n';
+                if (i + 1 < (size_t)len && data[i + 1] == '\n') ++i;
+            } else {
+                content[w++] = data[i];
+            }
+        }
+        content.resize(w);
+    } else {
+        content.assign(data, (size_t)len);
+    }
+    std::vector<long> caps;
+    const Str8 stripped = ruby_strip(content);
+    PASS("cc_flag", o.cc = c.R("cc_false_positive").search(stripped, 0, caps));
+    PASS("copyright_matcher", o.copyright = c.R("copyright_match").search(stripped, 0, caps));
+    Normalizer<Str8> nz{c, Str8()};
+    o.normalized8 = nz.run(content);
+    o.ascii = true;
+}
+
 void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* filename, bool is_file, FileOut& o) {
+    if (extname_is_html(filename)) { o.status = 1; return; }
+    if (c.ascii_path && all_ascii(data, (size_t)len)) {
+        prep_ascii(c, data, len, is_file, o);
+        return;
+    }
     Str content;
     PASS("decode", content = rx::from_utf8(data, (size_t)len));
     if (is_file) {   // universal newline (project_file.rb:41), in place
@@ -823,12 +925,11 @@ void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* file
     }
     for (char32_t ch : content)
         if (ch >= 0x80 && (c.unicode ? python_only(ch) : !safe_nonascii(ch))) { o.status = 1; return; }
-    if (extname_is_html(filename)) { o.status = 1; return; }
     std::vector<long> caps;
     const Str stripped = ruby_strip(content);
     PASS("cc_flag", o.cc = c.R("cc_false_positive").search(stripped, 0, caps));
     PASS("copyright_matcher", o.copyright = c.R("copyright_match").search(stripped, 0, caps));
-    Normalizer nz{c, Str()};
+    Normalizer<Str> nz{c, Str()};
     o.normalized = nz.run(content);
 }
 
@@ -880,6 +981,15 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
             const uint32_t h = spell_tok_slot(k[0], k[len - 1], len);
             c->spell_tok[h >> 6] |= 1ull << (h & 63);
         }
+        for (const auto& kv : c->spell) {
+            Str8 to;
+            for (char32_t ch : kv.second) {
+                if (ch >= 128) c->ascii_path = false;   // a non-ASCII replacement: UTF-32 only
+                to.push_back((char)ch);
+            }
+            c->spell_to8.push_back(to);
+        }
+        if (getenv("LH_NO_BYTE_PATH")) c->ascii_path = false;   // A/B and parity switch (tests)
         c->vocab.build(n_vocab, vocab);
         c->n_vocab = n_vocab;
         c->w64 = (n_vocab + 63) / 64;
@@ -959,7 +1069,7 @@ int64_t lh_normalize(lh_ctx* ctx, const char* data, int64_t len, const char* fil
     FileOut o;
     prep_one(*c, data, len, filename, is_file != 0, o);
     if (o.status) return -1;
-    const std::string u = rx::to_utf8(o.normalized);
+    const std::string u = o.ascii ? o.normalized8 : rx::to_utf8(o.normalized);
     if (out && cap > (int64_t)u.size()) {
         memcpy(out, u.data(), u.size());
         out[u.size()] = 0;
@@ -995,20 +1105,26 @@ int lh_prep_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t
                 // distinct words: vocabulary words are de-duplicated by their bit in `row`, the
                 // others through the per-thread WordSet
                 WordSet& words = tl_words;
-                words.reset(o.normalized);
-                PASS("wordset", scan_words(o.normalized, [&](size_t a, size_t b) {
-                    const char32_t* p = o.normalized.data() + a;
-                    const WordKey k = word_key(p, b - a, o.normalized.size() - a);
-                    const int32_t id = c->vocab.find(k, p);
-                    if (id >= 0) row[(size_t)id >> 6] |= 1ULL << (id & 63);
-                    else words.insert(a, k);
-                }));
+                auto scan = [&](const auto* text, size_t len) {
+                    words.reset(text);
+                    scan_words(text, len, [&](size_t a, size_t b) {
+                        const auto* p = text + a;
+                        const WordKey k = word_key(p, b - a, len - a);
+                        const int32_t id = c->vocab.find(k, p);
+                        if (id >= 0) row[(size_t)id >> 6] |= 1ULL << (id & 63);
+                        else words.insert(text, a, k);
+                    });
+                };
+                PASS("wordset", {
+                    if (o.ascii) scan(o.normalized8.data(), o.normalized8.size());
+                    else scan(o.normalized.data(), o.normalized.size());
+                });
                 size_t n_vocab_words = 0;
                 for (uint64_t wd : row) n_vocab_words += (size_t)__builtin_popcountll(wd);
                 const size_t n_words = n_vocab_words + words.count;
                 memcpy(bits + (size_t)f * c->w64, row.data(), sizeof(uint64_t) * (size_t)c->w64);
                 wf[f] = (uint32_t)n_words;
-                length[f] = (int32_t)o.normalized.size();
+                length[f] = (int32_t)(o.ascii ? o.normalized8.size() : o.normalized.size());
                 cc[f] = o.cc;
                 copyright[f] = o.copyright;
                 if (field_mask) {

@@ -325,8 +325,14 @@ thread_local size_t tl_match_depth = kDefaultMatchDepth;
 size_t max_match_depth() { return tl_match_depth; }
 void set_match_depth(size_t frames) { tl_match_depth = frames ? frames : kDefaultMatchDepth; }
 
+// text character i as a code point (a byte-path text is ASCII)
+static inline char32_t at(const char32_t* p, size_t i) { return p[i]; }
+static inline char32_t at(const char* p, size_t i) { return (unsigned char)p[i]; }
+
+template <class Ch>
 struct Matcher {
-    const Str& s;
+    const Ch* s;
+    size_t len;
     std::vector<long>& caps;
     // Continuation-passing backtracking nests one set of frames per matched node: a repeated
     // group such as the copyright pattern's (MAIN_LINE OPT*)+ goes deeper with every line it
@@ -346,13 +352,13 @@ struct Matcher {
     };
 
     bool lit(const Node* n, size_t pos) const {
-        if (pos >= s.size()) return false;
-        char32_t c = s[pos];
+        if (pos >= len) return false;
+        char32_t c = at(s, pos);
         return n->icase ? fold(c) == fold(n->ch) : c == n->ch;
     }
     bool cls(const Node* n, size_t pos) const {
-        if (pos >= s.size()) return false;
-        char32_t c = s[pos];
+        if (pos >= len) return false;
+        char32_t c = at(s, pos);
         bool in = false;
         for (auto& r : n->ranges) {
             if (c >= r.first && c <= r.second) { in = true; break; }
@@ -369,21 +375,21 @@ struct Matcher {
         const Guard g(depth, limit);
         switch (n->kind) {
             case Node::LIT: return lit(n, pos) && k(pos + 1);
-            case Node::ANY: return pos < s.size() && (n->dotall || s[pos] != '\n') && k(pos + 1);
+            case Node::ANY: return pos < len && (n->dotall || at(s, pos) != '\n') && k(pos + 1);
             case Node::CLASS: return cls(n, pos) && k(pos + 1);
-            case Node::BOL: return (pos == 0 || s[pos - 1] == '\n') && k(pos);
-            case Node::EOL: return (pos == s.size() || s[pos] == '\n') && k(pos);
+            case Node::BOL: return (pos == 0 || at(s, pos - 1) == '\n') && k(pos);
+            case Node::EOL: return (pos == len || at(s, pos) == '\n') && k(pos);
             case Node::BOS: return pos == 0 && k(pos);
-            case Node::EOS: return pos == s.size() && k(pos);
+            case Node::EOS: return pos == len && k(pos);
             case Node::WORDB: {
-                bool a = pos > 0 && is_word(s[pos - 1]), b = pos < s.size() && is_word(s[pos]);
+                bool a = pos > 0 && is_word(at(s, pos - 1)), b = pos < len && is_word(at(s, pos));
                 return a != b && k(pos);
             }
             case Node::SEQ: return seq(n, 0, pos, k);
             case Node::ALT: {
-                // branches that cannot start with s[pos] are skipped (first-character masks)
-                const char32_t c = pos < s.size() ? s[pos] : 0;
-                const bool end = pos >= s.size();
+                // branches that cannot start with at(s, pos) are skipped (first-character masks)
+                const char32_t c = pos < len ? at(s, pos) : 0;
+                const bool end = pos >= len;
                 for (size_t i = 0; i < n->kids.size(); ++i) {
                     if (!n->alt_nullable[i]) {
                         if (end) continue;
@@ -445,7 +451,7 @@ struct Matcher {
     bool single(const Node* n, size_t pos) const {
         switch (n->kind) {
             case Node::LIT: return lit(n, pos);
-            case Node::ANY: return pos < s.size() && (n->dotall || s[pos] != '\n');
+            case Node::ANY: return pos < len && (n->dotall || at(s, pos) != '\n');
             case Node::CLASS: return cls(n, pos);
             default: return false;
         }
@@ -641,18 +647,18 @@ static void required_runs(const Node* n, LitRun& cur, LitRun& best) {
 
 // first position >= from where req occurs (ASCII case folded when icase), or npos: candidates
 // by a vector scan for the literal's first and last characters (both cases when folded)
-static size_t find_required(const Str& s, size_t from, const Str& req, bool icase) {
-    const size_t m = req.size(), n = s.size();
+template <class C>
+static size_t find_required(const C* p, size_t n, size_t from, const Str& req, bool icase) {
+    const size_t m = req.size();
     if (m == 0) return from;
     if (n < m || from > n - m) return Str::npos;
     auto upper = [&](char32_t c) { return icase && c >= 'a' && c <= 'z' ? c - 32 : c; };
     const char32_t a = req[0], b = req[m - 1];
-    const char32_t* p = s.data();
     const size_t last = n - m;
     for (size_t i = scan::find_pair(p, from, last, m - 1, a, upper(a), b, upper(b)); i <= last;
          i = scan::find_pair(p, i + 1, last, m - 1, a, upper(a), b, upper(b))) {
         size_t k = 1;
-        while (k + 1 < m && (icase ? fold(p[i + k]) : p[i + k]) == req[k]) ++k;
+        while (k + 1 < m && (icase ? fold(at(p, i + k)) : at(p, i + k)) == req[k]) ++k;
         if (k + 1 >= m) return i;
     }
     return Str::npos;
@@ -719,16 +725,23 @@ Regex::Regex(const std::string& utf8, int flags) {
 }
 
 bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
+    return search_impl(s.data(), s.size(), start, caps);
+}
+
+bool Regex::search(const Str8& s, size_t start, std::vector<long>& caps) const {
+    return search_impl(s.data(), s.size(), start, caps);
+}
+
+template <class C>
+bool Regex::search_impl(const C* p, size_t n, size_t start, std::vector<long>& caps) const {
     caps.assign(2 * (ngroups_ + 1), -1);
     struct End : Cont { size_t* out; bool operator()(size_t e) const override { *out = e; return true; } } end;
     size_t e = 0;
     end.out = &e;
-    Matcher mt{s, caps};
-    const char32_t* p = s.data();
-    const size_t n = s.size();
+    Matcher<C> mt{p, n, caps};
     // a match at or after `start` contains req_ at or after `start` (anchored patterns are cheaper
     // to try at their few start positions)
-    if (!anchored_ && !line_anchored_ && !req_.empty() && find_required(s, start, req_, req_icase_) == Str::npos)
+    if (!anchored_ && !line_anchored_ && !req_.empty() && find_required(p, n, start, req_, req_icase_) == Str::npos)
         return false;
     auto first_ok = [&](char32_t c) { return c < 128 ? first_[c] != 0 : first_nonascii_; };
     for (size_t pos = start; pos <= n; ++pos) {
@@ -740,7 +753,7 @@ bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
                 pos = j + 1;
             }
             // a match starts with one of the first characters: else try the next line
-            if (has_first_ && (pos == n || !first_ok(p[pos]))) {
+            if (has_first_ && (pos == n || !first_ok(at(p, pos)))) {
                 if (pos == n) return false;
                 continue;
             }
@@ -749,7 +762,7 @@ bool Regex::search(const Str& s, size_t start, std::vector<long>& caps) const {
             if (n_first_list_) {
                 pos = scan::find_any(p, pos, n, first_list_, n_first_list_);
             } else {
-                while (pos < n && !first_ok(p[pos])) ++pos;
+                while (pos < n && !first_ok(at(p, pos))) ++pos;
             }
             if (pos == n) return false;
         }
@@ -769,11 +782,22 @@ bool Regex::sub_into(Str& s, const Str& repl) const {
     return true;
 }
 
-Str Regex::sub(const Str& s, const Str& repl, bool* changed) const {
+bool Regex::sub_into(Str8& s, const Str8& repl) const {
+    std::vector<long> caps;
+    if (!search(s, 0, caps)) return false;
+    s = sub(s, repl);
+    return true;
+}
+
+Str Regex::sub(const Str& s, const Str& repl, bool* changed) const { return sub_impl(s, repl, changed); }
+Str8 Regex::sub(const Str8& s, const Str8& repl, bool* changed) const { return sub_impl(s, repl, changed); }
+
+template <class S>
+S Regex::sub_impl(const S& s, const S& repl, bool* changed) const {
     bool any = false;
-    Str out = sub_fn(s, [&](const Str& src, const std::vector<long>& caps) {
+    S out = sub_fn(s, [&](const S& src, const std::vector<long>& caps) {
         any = true;
-        Str r;
+        S r;
         for (size_t i = 0; i < repl.size(); ++i) {
             if (repl[i] == '\\' && i + 1 < repl.size() && repl[i + 1] >= '0' && repl[i + 1] <= '9') {
                 int g = (int)(repl[i + 1] - '0');

@@ -18,6 +18,9 @@
 namespace rx {
 
 using Str = std::u32string;
+// A text whose every character is ASCII, one byte per character (the byte path of
+// normalize.cpp: the same patterns, matched over 4x fewer bytes)
+using Str8 = std::string;
 
 enum Flags : int { IGNORECASE = 2, MULTILINE = 8, DOTALL = 16 };  // Python re flag values
 
@@ -59,14 +62,17 @@ public:
     Regex(const std::string& utf8_pattern, int flags);
     // search from `start`; on success fills caps ([2*i], [2*i+1]; -1 when unset) for i <= ngroups
     bool search(const Str& s, size_t start, std::vector<long>& caps) const;
+    bool search(const Str8& s, size_t start, std::vector<long>& caps) const;
     int ngroups() const { return ngroups_; }
     bool anchored() const { return anchored_; }
     // re.sub with a template supporting \1..\9 (and literal text); count = 0 -> all
     Str sub(const Str& s, const Str& repl, bool* changed = nullptr) const;
+    Str8 sub(const Str8& s, const Str8& repl, bool* changed = nullptr) const;
     // in-place re.sub: returns false (s untouched, no copy) when nothing matches
     bool sub_into(Str& s, const Str& repl) const;
-    template <class F>
-    Str sub_fn(const Str& s, F&& fn) const;  // replacement computed from the match
+    bool sub_into(Str8& s, const Str8& repl) const;
+    template <class S, class F>
+    S sub_fn(const S& s, F&& fn) const;  // replacement computed from the match
     bool valid() const { return (bool)root_; }
 
 private:
@@ -81,6 +87,11 @@ private:
     int n_first_list_ = 0;            // (vector scan; 0: use first_)
     Str req_;                         // a literal every match contains (empty: none found)
     bool req_icase_ = false;          // ... compared with ASCII case folding
+    template <class C>
+    bool search_impl(const C* p, size_t n, size_t start, std::vector<long>& caps) const;
+    template <class S>
+    S sub_impl(const S& s, const S& repl, bool* changed) const;
+    template <class C>
     friend struct Matcher;
 };
 
@@ -97,9 +108,9 @@ bool is_word_char(char32_t c);
 
 // ---- template implementation ---------------------------------------------------------
 namespace rx {
-template <class F>
-Str Regex::sub_fn(const Str& s, F&& fn) const {
-    Str out;
+template <class S, class F>
+S Regex::sub_fn(const S& s, F&& fn) const {
+    S out;
     size_t pos = 0, last = 0;
     std::vector<long> caps;
     while (pos <= s.size() && search(s, pos, caps)) {
@@ -111,7 +122,7 @@ Str Regex::sub_fn(const Str& s, F&& fn) const {
         if (me == ms && ms < s.size()) out.push_back(s[ms]), last = ms + 1;
         if (anchored_) break;
     }
-    if (last < s.size()) out.append(s, last, Str::npos);
+    if (last < s.size()) out.append(s, last, S::npos);
     return out;
 }
 }  // namespace rx

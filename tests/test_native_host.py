@@ -247,3 +247,34 @@ def test_thousands_of_copyright_lines(hp):
     # single-text entry point on this (8 MiB) thread: small texts native, the deep one falls back
     assert hp.normalize(texts[0]) == LicenseFile(texts[0], 'LICENSE').content_normalized()
     assert hp.normalize(texts[2]) is None
+
+
+def test_byte_path_equals_utf32_path(hp, monkeypatch):
+    """ASCII texts are normalized as bytes (normalize.cpp prep_ascii); LH_NO_BYTE_PATH=1 sends
+    them through the UTF-32 passes instead. Both paths give identical batch outputs on ASCII
+    fuzz texts, the template bodies and texts with CR / CRLF line ends."""
+    from licensee_amd.native_host import HostPrep
+    monkeypatch.setenv('LH_NO_BYTE_PATH', '1')
+    wide = HostPrep(hp.corpus)
+    monkeypatch.delenv('LH_NO_BYTE_PATH')
+    rng = random.Random(11)
+    ascii_frags = [f for f in FRAGMENTS if f.isascii()]
+    bodies = [t.content_normalized() for t in License.all(hidden=True, pseudo=False)]
+    texts = []
+    for i in range(600):
+        parts = [rng.choice(ascii_frags) for _ in range(rng.randint(1, 20))]
+        text = rng.choice(['\n', '\r\n', '\r', ' ']).join(parts)
+        if rng.random() < 0.5:
+            b = rng.choice(bodies)
+            text += '\n\n' + b[:rng.randint(0, len(b))]
+        texts.append(text)
+    texts += bodies + ['', ' ', '\r', 'a' * 40 + '-' + 'b' * 40]
+    names = ['LICENSE'] * len(texts)
+    a = hp.prep_files(texts, names, nthreads=4)
+    b = wide.prep_files(texts, names, nthreads=4)
+    assert not a[3].any() and not b[3].any()
+    for field in ('bits', 'wordset_size', 'length', 'cc_false_positive'):
+        assert np.array_equal(getattr(a[0], field), getattr(b[0], field)), field
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    for t in texts[:200]:
+        assert hp.normalize(t, 'LICENSE') == wide.normalize(t, 'LICENSE')
