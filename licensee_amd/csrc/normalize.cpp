@@ -412,6 +412,11 @@ struct Ctx {
     std::vector<int32_t> spell_trie;
     std::vector<int32_t> spell_key;
     uint64_t spell_tok[(1u << 15) / 64] = {};   // spell_tok_slot of every key's first \w run
+    // byte path: the keys' first three bytes as a nibble fingerprint (spell_prefix_mask): 8
+    // buckets; teddy[k][0|1][nibble] = the buckets with a key whose byte k has that low | high
+    // nibble (16 entries repeated for both 128-bit lanes)
+    alignas(32) uint8_t teddy[3][2][32] = {};
+    bool teddy_ok = true;
     // Unicode tables (lh_set_unicode): Python str.lower() of non-ASCII code points
     bool unicode = false;
     std::unordered_map<char32_t, char32_t> lower;
@@ -551,6 +556,10 @@ struct Normalizer {
             }
             uint64_t starts = w & ~((w << 1) | prev_word);
             prev_word = w >> 63;
+#if defined(__AVX2__)
+            if constexpr (sizeof(C) == 1)
+                if (c.teddy_ok && starts) starts &= spell_prefix_mask(p + b0, n - b0);
+#endif
             while (starts) {
                 const size_t off = (size_t)__builtin_ctzll(starts);
                 starts &= starts - 1;
@@ -581,6 +590,32 @@ struct Normalizer {
         cur.swap(out);
         clean = false;
     }
+#if defined(__AVX2__)
+    // Bit j: some key could start at q[j] -- its first three bytes pass the nibble fingerprint
+    // (no false negatives; q[j + 1], q[j + 2] past the text read as 0, which no key holds).
+    uint64_t spell_prefix_mask(const char* q, size_t avail) const {
+        alignas(32) char pad[96];
+        if (avail < 66) {
+            memset(pad, 0, sizeof pad);
+            memcpy(pad, q, avail);
+            q = pad;
+        }
+        const __m256i nib = _mm256_set1_epi8(0x0f);
+        uint64_t m = 0;
+        for (int h = 0; h < 64; h += 32) {
+            __m256i r = _mm256_set1_epi8(-1);
+            for (int k = 0; k < 3; ++k) {
+                const __m256i x = _mm256_loadu_si256((const __m256i*)(q + h + k));
+                const __m256i lo = _mm256_shuffle_epi8(_mm256_load_si256((const __m256i*)c.teddy[k][0]), _mm256_and_si256(x, nib));
+                const __m256i hi = _mm256_shuffle_epi8(_mm256_load_si256((const __m256i*)c.teddy[k][1]),
+                                                       _mm256_and_si256(_mm256_srli_epi16(x, 4), nib));
+                r = _mm256_and_si256(r, _mm256_and_si256(lo, hi));
+            }
+            m |= (uint64_t)(uint32_t)~_mm256_movemask_epi8(_mm256_cmpeq_epi8(r, _mm256_setzero_si256())) << h;
+        }
+        return m;
+    }
+#endif
     bool spell_tok_hit(char32_t first, char32_t last, size_t len) const {
         const uint32_t h = spell_tok_slot(first, last, len);
         return (c.spell_tok[h >> 6] >> (h & 63)) & 1;
@@ -671,9 +706,14 @@ struct Normalizer {
             if (amps) {
                 S out;
                 out.reserve(cur.size() + 2 * amps);
-                for (C ch : cur) {
-                    if (ch == '&') out += LIT("and");
-                    else out.push_back(ch);
+                const C* p = cur.data();
+                const size_t n = cur.size();
+                for (size_t i = 0;;) {
+                    const size_t e = scan::find_char(p, i, n, U'&');
+                    out.append(p + i, e - i);
+                    if (e == n) break;
+                    out += LIT("and");
+                    i = e + 1;
                 }
                 cur.swap(out);
             }
@@ -961,6 +1001,25 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
             }
         }
         if (nsym > kSpellSyms) throw std::runtime_error("spelling keys: alphabet too large");
+        {   // the byte path's prefix fingerprint: distinct 3-byte prefixes, sorted, in 8 runs
+            std::vector<Str> pre;
+            for (const auto& kv : c->spell) {
+                if (kv.first.size() < 3) c->teddy_ok = false;
+                else pre.push_back(kv.first.substr(0, 3));
+            }
+            std::sort(pre.begin(), pre.end());
+            pre.erase(std::unique(pre.begin(), pre.end()), pre.end());
+            for (size_t j = 0; j < pre.size(); ++j) {
+                const uint8_t bit = (uint8_t)(1u << (j * 8 / pre.size()));
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t ch = (uint32_t)pre[j][(size_t)k];   // ASCII (checked above)
+                    for (int lane = 0; lane < 32; lane += 16) {
+                        c->teddy[k][0][lane + (ch & 15)] |= bit;
+                        c->teddy[k][1][lane + (ch >> 4)] |= bit;
+                    }
+                }
+            }
+        }
         c->spell_trie.assign(kSpellSyms, 0);
         c->spell_key.assign(1, -1);
         for (int32_t i = 0; i < n_spell; ++i) {
