@@ -278,3 +278,20 @@ def test_byte_path_equals_utf32_path(hp, monkeypatch):
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
     for t in texts[:200]:
         assert hp.normalize(t, 'LICENSE') == wide.normalize(t, 'LICENSE')
+
+
+def test_spelling_keys_at_block_edges(hp):
+    """The byte path's spelling prefilter (normalize.cpp spell_prefix_mask) reads 64-byte blocks
+    and a zero-padded copy near the text's end: every key at every offset around the block and
+    half-block edges and at the very end of the text is still replaced."""
+    from licensee_amd.content_helper import VARIETAL_WORDS
+    checked = 0
+    for key in VARIETAL_WORDS:
+        for off in (0, 1, 29, 30, 31, 32, 33, 61, 62, 63, 64, 65, 95, 96, 127, 128):
+            filler = ('ab ' * 64)[:off]
+            for tail in ('', ' end', ' ' + 'z' * 70):
+                text = filler + key + tail
+                got = hp.normalize(text, 'LICENSE')
+                assert got == LicenseFile(text, 'LICENSE').content_normalized(), (key, off, tail)
+                checked += 1
+    assert checked == len(VARIETAL_WORDS) * 16 * 3
