@@ -665,6 +665,42 @@ struct Normalizer {
         ascii_done_ = i;
     }
 
+    // border_markup ^[*-](.*?)[*-]$ -> \1 (content_helper.rb:17, :98): '.' stops at '\n' and '$' holds
+    // only before '\n' or at the end, so a match is a whole line of >= 2 characters that starts and
+    // ends with '*' or '-', and the replacement drops those two characters. Line starts holding
+    // '*' / '-' are found by a vector pair search; lines that match are then compacted in place.
+    void strip_borders() {
+        C* p = cur.data();
+        const size_t n = cur.size();
+        if (n < 2) return;
+        auto border = [](C ch) { return ch == '*' || ch == '-'; };
+        std::vector<std::pair<size_t, size_t>> lines;   // matching lines [a, e)
+        auto check = [&](size_t a) {
+            const size_t e = scan::find_char(p, a, n, U'\n');
+            if (e - a >= 2 && border(p[e - 1])) lines.emplace_back(a, e);
+            return e;
+        };
+        size_t from = 0;
+        if (border(p[0])) from = check(0);
+        while (from + 1 < n) {
+            const size_t i = scan::find_pair(p, from, n - 2, 1, U'\n', U'\n', U'*', U'-');
+            if (i > n - 2) break;
+            from = check(i + 1);
+        }
+        if (lines.empty()) return;
+        size_t w = lines[0].first;
+        for (size_t j = 0; j < lines.size(); ++j) {
+            const size_t a = lines[j].first, e = lines[j].second;
+            const size_t next = j + 1 < lines.size() ? lines[j + 1].first : n;
+            memmove(p + w, p + a + 1, (e - a - 2) * sizeof(C));   // the line without its borders
+            w += e - a - 2;
+            memmove(p + w, p + e, (next - e) * sizeof(C));        // '\n' and the lines up to the next match
+            w += next - e;
+        }
+        cur.resize(w);
+        clean = false;
+    }
+
     // strip(:whitespace): gsub(/\s+/, ' ').squeeze(' ').strip, in place
     void collapse_whitespace() {
         cur.resize(scan::squeeze_runs(cur.data(), 0, 0, cur.size(), false, true));
@@ -760,7 +796,7 @@ struct Normalizer {
             strip_re(c.R("cc0_disclaimer"));
         });
         PASS("unlicense_optional", if (contains(cur, LIT("unlicense"))) strip_re(c.R("unlicense_info")));
-        PASS("borders", sub_re(c.R("border_markup"), LIT("\\1")));
+        PASS("borders", strip_borders());
         PASS("title2", strip_title());
         PASS("version2", strip_re(c.R("version")));
         PASS("url", strip_re(c.R("url")));

@@ -295,3 +295,23 @@ def test_spelling_keys_at_block_edges(hp):
                 assert got == LicenseFile(text, 'LICENSE').content_normalized(), (key, off, tail)
                 checked += 1
     assert checked == len(VARIETAL_WORDS) * 16 * 3
+
+
+def test_border_lines_fuzz(hp):
+    """The hand-written border_markup pass (normalize.cpp strip_borders: ^[*-](.*?)[*-]$ -> \\1)
+    on texts dense in lines that start and/or end with '*' / '-', on both text paths."""
+    rng = random.Random(7)
+    pieces = ['*', '-', '--', '**', '*-', '-*', '* x *', '- item -', '-x', 'x-', '*x', 'x*', '---', '- a', 'b -',
+              '* * *', ' * y *', '-- z --', 'plain line', '', 'licence - x', '*é*', '- café -']
+    checked = 0
+    for i in range(500):
+        lines = [rng.choice(pieces) for _ in range(rng.randint(1, 25))]
+        text = rng.choice(['\n', '\n\n']).join(lines)
+        if rng.random() < 0.3:
+            text = 'The MIT License\n\n' + text + '\n\nPermission is granted.'
+        got = hp.normalize(text, 'LICENSE')
+        if got is None:
+            continue
+        checked += 1
+        assert got == LicenseFile(text, 'LICENSE').content_normalized(), (i, text[:300])
+    assert checked > 450
