@@ -24,6 +24,6 @@ for r in $(seq 1 "$REPS"); do
     out=gpurun_out/ab/${tag}_r$r
     env $envs timeout -k 10 300 python bench.py $ARGS --warmup 2 --extra-configs= --no-cpu-baseline --no-extras \
       > $out.json 2> $out.err || { echo "$arm r$r failed (rc $?)"; exit 3; }
-    python -c "import json;d=json.load(open('$out.json'));r=d['roofline'];print('$arm r$r', round(r['launch_ms'],4), 'ms frac', round(r['frac'],3))"
+    python -c "import json;d=json.load(open('$out.json'));r=d['roofline'];print('$arm r$r', round(r['launch_ms'],4), 'ms frac', round(r['frac'],3), 'parity', d.get('parity'))"
   done
 done
