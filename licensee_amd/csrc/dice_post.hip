@@ -45,7 +45,8 @@ namespace dice {
 
 // Phase-skip diagnostics (tools/build_variant.sh -DPOST_DIAG=n; results are wrong): 1 skips the
 // dense kernel, 2 the postings walk, 4 the narrow-word extraction, 8 scoring. (Round 6's fusion-cost
-// probe, 16 / 48, is in the history: profiles/r6_fusion_probe.txt)
+// probe, 16 / 48, and the matrix kernel with walk and store waves are in the history:
+// profiles/r6_fusion_probe.txt, profiles/r6_store_waves_ab.txt)
 #ifndef POST_DIAG
 #define POST_DIAG 0
 #endif
@@ -807,155 +808,6 @@ __global__ __launch_bounds__(kNarrowWavesMatrix * kWave) __attribute__((amdgpu_w
                                   score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn, ld);
 }
 
-// ---- the matrix kernel with walk and store waves ------------------------------------------
-// Full-matrix mode writes 12 bytes per (file, template) -- 7.3 KB per config-3 file, 9 GB per
-// 5-T600 launch -- and gfx950's vmcnt counts stores as well as loads, in order: in the uniform
-// kernel a wave's next file's first row loads waited for the previous file's ~20 row stores
-// (1.03 of 4.58 ms went to them). Here the roles are split inside a workgroup of
-// NWALK + NSTORE waves. Walk waves take the tile's files (walk wave w: files w, w + NWALK, ...),
-// build each counter row (file_postings: dense partials copied in, narrow words queued and
-// walked) and hand it over; they issue no global store. Store waves score the handed-over rows
-// (score_file: the same code as the uniform kernel) and issue every row, score and top-k store;
-// they issue no global load, so nothing they wait for (LDS reads: lgkmcnt) queues behind their
-// stores. Each walk wave has two counter rows: while store wave w % NSTORE scores row b, the walk
-// wave builds the next file in row b ^ 1. Handover, per walk wave, in LDS: ready = files
-// published, freed = files whose row the store waves have finished reading; file k uses row
-// k & 1 and waits for freed >= k - 1. Publishing and freeing wait for the wave's own LDS traffic
-// (lgkmcnt(0): the walk's atomics have landed / the row's reads have returned) and then write the
-// counter; LDS operations of one wave are performed in order. Persistent workgroups (the pipeline
-// stays full across tiles); every wait is bounded (kSpinCap sleeps), so the grid drains whatever
-// happens. A walk wave ends with an end marker (file 0xFFFFFFFF) in its next row's info slot.
-constexpr uint32_t kWsEnd = 0xFFFFFFFFu;
-constexpr uint32_t kSpinCap = 1u << 22;   // ~0.3 s of s_sleep 1: far past any real wait
-
-__device__ __forceinline__ uint32_t lds_peek(const uint32_t* p) {
-    return rfl(__hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_publish(uint32_t* p, uint32_t v) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// wait until *p >= v (false: the spin cap was hit)
-__device__ __forceinline__ bool lds_wait_ge(const uint32_t* p, uint32_t v) {
-    for (uint32_t i = 0; i < kSpinCap; ++i) {
-        if (lds_peek(p) >= v) {
-            asm volatile("" ::: "memory");
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-template <int TPMAX, int NWALK, int NSTORE>
-__device__ __forceinline__ void post_matrix_ws_body(POST_NARROW_ARGS) {
-    constexpr int kTJ = (TPMAX + kWave - 1) / kWave;
-    constexpr int kWCap = word_cap<TPMAX>();
-    constexpr int kPJ = pairs_per_lane<TPMAX>();
-    constexpr int kServe = NWALK / NSTORE;   // walk waves per store wave
-    static_assert(NWALK % NSTORE == 0 && kServe <= 5, "store waves serve whole walk waves");
-    // two u32 counter rows per walk wave, then the walk waves' word queues (the walk's sinks lie
-    // past every row and within 64 KiB of its wave's rows: wave 0 has the largest gap)
-    __shared__ uint32_t cntq[2 * NWALK * TPMAX + NWALK * kWCap];
-    static_assert((2 * NWALK * TPMAX + kWCap) * 4 <= 0xFFFE, "sinks within reach of every row");
-    __shared__ uint2 tcs[TPMAX];
-    __shared__ uint2 lq[NWALK][kLongCap];
-    __shared__ uint4 info[NWALK][2];   // per row: {file, |W_F|, len_F, cc}
-    __shared__ uint32_t ready[NWALK], freed[NWALK];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = (int)rfl(threadIdx.x >> 6);
-    for (int i = threadIdx.x; i < T; i += (NWALK + NSTORE) * kWave) tcs[i] = tc[i];
-    for (int i = threadIdx.x; i < 2 * NWALK * TPMAX; i += (NWALK + NSTORE) * kWave) cntq[i] = 0;
-    if (threadIdx.x < NWALK) ready[threadIdx.x] = freed[threadIdx.x] = 0;
-    __syncthreads();
-
-    if (wave < NWALK) {
-        uint32_t* const wq = cntq + 2 * NWALK * TPMAX + wave * kWCap;
-        const int32_t pb0 = (POST_DIAG & 4) ? w64 : D;
-        uint32_t pub = 0;   // files published
-        for (int64_t f0 = (int64_t)blockIdx.x * kPostFiles; f0 < n; f0 += (int64_t)gridDim.x * kPostFiles) {
-            const int64_t rem64 = n - f0;
-            const int32_t nt = (rem64 >> 32) != 0 || (uint32_t)rem64 >= (uint32_t)kPostFiles ? kPostFiles : (int32_t)rem64;
-            const int64_t tpos = f0 + min(lane, nt - 1);
-            const uint32_t twf = wfp[tpos];
-            const uint32_t tlen = (uint32_t)lenp[tpos];
-            const uint64_t tcc = __ballot(ccp[tpos] != 0);
-            for (int fi = wave; fi < nt; fi += NWALK) {
-                const int64_t pos = f0 + fi;
-                int32_t tpf = tp;
-                int lanef = lane;
-                asm volatile("" : "+s"(tpf), "+v"(lanef));
-                if (pub >= 2) lds_wait_ge(&freed[wave], pub - 1);   // row pub & 1 read by the store waves
-                uint32_t* crow32 = cntq + (2 * wave + (int)(pub & 1)) * TPMAX;
-                file_postings<kWCap, true, kPJ>(rows + pos * w64, w64, pb0, part16, pos, tpf, wq, lq[wave], prow, plong,
-                                                crow32, lanef);
-                if (lane == 0)
-                    info[wave][pub & 1] = make_uint4((uint32_t)pos, rfl(__builtin_amdgcn_readlane(twf, fi)),
-                                                   rfl(__builtin_amdgcn_readlane(tlen, fi)), (uint32_t)((tcc >> fi) & 1u));
-                ++pub;
-                if (lane == 0) lds_publish(&ready[wave], pub);
-            }
-        }
-        if (pub >= 2) lds_wait_ge(&freed[wave], pub - 1);
-        if (lane == 0) {
-            info[wave][pub & 1] = make_uint4(kWsEnd, 0, 0, 0);
-            lds_publish(&ready[wave], pub + 1);
-        }
-        return;
-    }
-    // store wave s serves walk waves s, s + NSTORE, ...: whichever has a row ready
-    const int s = wave - NWALK;
-    uint32_t taken[kServe];   // files consumed per served walk wave
-#pragma unroll
-    for (int j = 0; j < kServe; ++j) taken[j] = 0;
-    uint32_t live = (1u << kServe) - 1;
-    uint32_t idle = 0;
-    while (live && idle < kSpinCap) {
-        int pick = -1;
-        uint32_t kk = 0;
-#pragma unroll
-        for (int j = 0; j < kServe; ++j)
-            if (pick < 0 && ((live >> j) & 1u) && lds_peek(&ready[s + j * NSTORE]) > taken[j]) {
-                pick = j;
-                kk = taken[j];
-            }
-        if (pick < 0) {
-            __builtin_amdgcn_s_sleep(1);
-            ++idle;
-            continue;
-        }
-        asm volatile("" ::: "memory");
-        idle = 0;
-        const int w = s + pick * NSTORE;
-        const uint4 inf = info[w][kk & 1];
-        if (rfl(inf.x) == kWsEnd) {
-            live &= ~(1u << pick);
-            continue;
-        }
-        int32_t Tf = T, ldf = ld;
-        int lanef = lane;
-        asm volatile("" : "+s"(Tf), "+s"(ldf), "+v"(lanef));
-        uint32_t* crow32 = cntq + (2 * w + (int)(kk & 1)) * TPMAX;
-        if (!(POST_DIAG & 8))
-            score_file<true, kTJ>(crow32, tcs, Tf, ldf, (int64_t)rfl(inf.x), rfl(inf.y), (int32_t)rfl(inf.z),
-                                  rfl(inf.w) != 0, corpus_fast, thr, best_out, ov_out, score_out, k, mov, msc, tki, tks,
-                                  lanef);
-#pragma unroll
-        for (int j = 0; j < kServe; ++j)
-            if (j == pick) taken[j] = kk + 1;
-        if (lane == 0) lds_publish(&freed[w], kk + 1);
-    }
-}
-
-// NWALK + NSTORE waves per workgroup, WGS workgroups per CU (LDS: two counter rows per walk wave)
-template <int TPMAX, int NWALK, int NSTORE, int WGS>
-__global__ __launch_bounds__((NWALK + NSTORE) * kWave) __attribute__((amdgpu_waves_per_eu(
-    (NWALK + NSTORE) * WGS / 4, (NWALK + NSTORE) * WGS / 4))) void dice_post_narrow_matrix_ws(POST_NARROW_ARGS) {
-    post_matrix_ws_body<TPMAX, NWALK, NSTORE>(rows, n, w64, D, T, tp, part16, prow, plong, tc, wfp, lenp, ccp, thr,
-                                              best_out, ov_out, score_out, k, mov, msc, tki, tks, corpus_fast, idx, pn,
-                                              ld);
-}
-
 // ---- host side ---------------------------------------------------------------------------
 
 // Estimated per-file cost (wave instructions) of a dense prefix of D u64 words: the matrix-core
@@ -1155,38 +1007,7 @@ static int launch(dice_ctx* c, dice_batch* b, double thr, int32_t k, hipStream_t
     }
     auto kern = c->post_tp <= 608 ? (kMatrix ? dice_post_narrow_matrix<608> : dice_post_narrow_match<608>)
                                   : (kMatrix ? dice_post_narrow_matrix<kPostMaxTpad> : dice_post_narrow_match<kPostMaxTpad>);
-    int64_t grid = groups;
-    int threads = kNarrowWaves * kWave;
-    if constexpr (kMatrix) {   // (A/B during development) walk/store wave split
-        const char* ws = getenv("DICE_POST_WS");
-        const std::string v = ws ? ws : "8x4";
-        const bool small = c->post_tp <= 608;
-        int wgs = 0;
-        if (v == "8x4") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 8, 4, 2> : dice_post_narrow_matrix_ws<kPostMaxTpad, 8, 4, 2>;
-            threads = 12 * kWave, wgs = 2;
-        } else if (v == "6x2") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 6, 2, 3> : dice_post_narrow_matrix_ws<kPostMaxTpad, 6, 2, 3>;
-            threads = 8 * kWave, wgs = 3;
-        } else if (v == "8x8") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 8, 8, 2> : dice_post_narrow_matrix_ws<kPostMaxTpad, 8, 8, 2>;
-            threads = 16 * kWave, wgs = 2;
-        } else if (v == "6x6") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 6, 6, 3> : dice_post_narrow_matrix_ws<kPostMaxTpad, 6, 6, 3>;
-            threads = 12 * kWave, wgs = 3;
-        } else if (v == "4x4") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 4, 4, 4> : dice_post_narrow_matrix_ws<kPostMaxTpad, 4, 4, 4>;
-            threads = 8 * kWave, wgs = 4;
-        } else if (v == "9x3") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 9, 3, 2> : dice_post_narrow_matrix_ws<kPostMaxTpad, 9, 3, 2>;
-            threads = 12 * kWave, wgs = 2;
-        } else if (v == "10x2") {
-            kern = small ? dice_post_narrow_matrix_ws<608, 10, 2, 2> : dice_post_narrow_matrix_ws<kPostMaxTpad, 10, 2, 2>;
-            threads = 12 * kWave, wgs = 2;
-        }
-        if (wgs) grid = std::min<int64_t>(tiles, (int64_t)wgs * c->n_cu);
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), 0, s,
+    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kNarrowWaves * kWave), 0, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, c->post_dense, c->T, c->post_tp,
                        part16, (const uint16_t*)c->d_prow, (const uint16_t*)c->d_povf,
                        (const uint2*)c->d_ptc, b->d_wf, b->d_len, b->d_cc, thr, b->d_best, b->d_ov, b->d_score, k,
