@@ -839,34 +839,63 @@ inline size_t word_end(const C* s, size_t i, size_t n) {
 
 // Tokens are the runs of [\w/-] (64-character masks), except that a run followed by '\'' is
 // re-scanned by the regex's loop ('s and s' continue a token; an apostrophe never starts one).
-// A token ends at a character outside [\w/-], so the next one starts at a run start.
+// Per 64-character block the run starts and the run ends (the non-word character after a run)
+// come from the mask, and the k-th start pairs with the k-th end; a token whose run continues
+// past the block stays open until the next block's first end. A re-scanned token that ends past
+// its run consumed the starts and ends before its end (resume).
 template <class C, class F>
 void scan_words(const C* p, size_t n, F&& emit) {
-    size_t resume = 0;   // end of the last token
     uint64_t prev = 0;
-    for (size_t b0 = 0; b0 < n; b0 += 64) {
+    size_t open = SIZE_MAX;   // start of a token whose run continues past the block
+    size_t resume = 0;        // after a re-scan: tokens start at or after it
+    uint64_t starts = 0, ends = 0;
+    size_t b0 = 0;
+    auto finish = [&](size_t a, size_t e) {
+        if (__builtin_expect(e < n && p[e] == '\'', 0)) {
+            const size_t e2 = word_end(p, a, n);
+            if (e2 > e) {
+                resume = e2;
+                const size_t r = e2 - b0;
+                starts = r >= 64 ? 0 : starts & (~0ULL << r);
+                ends = r >= 63 ? 0 : ends & (~0ULL << (r + 1));   // a run end at e2 is the token's own
+            }
+            e = e2;
+        }
+        emit(a, e);
+    };
+    for (; b0 < n; b0 += 64) {
         uint64_t hi;
         const uint64_t w = scan::ascii_word_mask<true>(p + b0, std::min<size_t>(64, n - b0), &hi);
-        uint64_t starts = w & ~((w << 1) | prev);
+        const uint64_t wp = (w << 1) | prev;
+        starts = w & ~wp;
+        ends = ~w & wp;
         prev = w >> 63;
+        if (__builtin_expect(resume >= b0, 0)) {
+            const size_t r = resume - b0;
+            if (r >= 64) continue;
+            starts &= ~0ULL << r;
+            ends &= r >= 63 ? 0 : ~0ULL << (r + 1);
+        }
+        if (open != SIZE_MAX) {
+            if (!ends) continue;
+            const size_t e = b0 + (size_t)__builtin_ctzll(ends);
+            ends &= ends - 1;
+            finish(open, e);
+            open = SIZE_MAX;
+        }
         while (starts) {
-            const size_t off = (size_t)__builtin_ctzll(starts);
+            const size_t a = b0 + (size_t)__builtin_ctzll(starts);
             starts &= starts - 1;
-            const size_t a = b0 + off;
-            if (a < resume) continue;
-            const uint64_t rest = ~w >> off;
-            size_t e;
-            if (rest) {
-                e = std::min(n, a + (size_t)__builtin_ctzll(rest));
-            } else {
-                e = b0 + 64;
-                while (e < n && wchar(cp(p[e]))) ++e;
+            if (!ends) {
+                open = a;
+                break;
             }
-            if (e < n && p[e] == '\'') e = word_end(p, a, n);
-            emit(a, e);
-            resume = e;
+            const size_t e = b0 + (size_t)__builtin_ctzll(ends);
+            ends &= ends - 1;
+            finish(a, e);
         }
     }
+    if (open != SIZE_MAX) emit(open, n);
 }
 
 bool extname_is_html(const char* fn) {

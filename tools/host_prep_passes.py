@@ -21,7 +21,7 @@ def main():
     march = os.environ.get('LH_MARCH', 'x86-64-v3')
     csrc = os.path.join(ROOT, 'licensee_amd', 'csrc')
     so = '/tmp/liblicensee_host_timing.so'
-    subprocess.run(['g++', '-O3', f'-march={march}', '-std=c++17', '-fPIC', '-shared', '-pthread', '-DLH_PASS_TIMING', '-o', so] +
+    subprocess.run(['g++', '-O3', f'-march={march}', '-std=c++17', '-fPIC', '-shared', '-pthread', '-DLH_PASS_TIMING', *os.environ.get('LH_FLAGS','').split(), '-o', so] +
                    [os.path.join(csrc, f) for f in ('rx.cpp', 'normalize.cpp', 'vocab_pack.cpp')], check=True)
     import ctypes
     from licensee_amd import native_host
