@@ -786,25 +786,52 @@ def main():
         t_h = time.perf_counter()
         hp.prep_files(big, None, nthreads=nthreads)
         extras['host_prep_native_files_per_s'] = len(big) / (time.perf_counter() - t_h)
+        # the host stage when the device scans the wordsets (lh_normalize_files: decode,
+        # content_normalized, CC flag, Copyright), and the device scan itself (dice_batch_upload_text:
+        # H2D of the texts + dice_words_kernel + status read-back + repack, wall time)
+        hp.normalize_files(big[:256], None, nthreads=nthreads)
+        t_h = time.perf_counter()
+        norm = hp.normalize_files(big, None, nthreads=nthreads)
+        extras['host_normalize_files_per_s'] = len(big) / (time.perf_counter() - t_h)
+        if run.cfg == 2:
+            run.scorer.vocab_setup(corpus.vocab, hp.nv_fields)
+            wb = run.scorer.batch(len(big))
+            text, off, tl, ln, ccf, _, _ = norm
+            wb.upload_text(text, off, tl, ln, ccf)
+            reps = []
+            for _ in range(3):
+                t_h = time.perf_counter()
+                wb.upload_text(text, off, tl, ln, ccf)
+                reps.append(time.perf_counter() - t_h)
+            extras['device_wordset_files_per_s'] = len(big) / sorted(reps)[1]
+            extras['device_wordset_note'] = (f'dice_batch_upload_text over the {len(big)} normalized texts '
+                                             f'({len(text) / len(big) / 1024:.1f} KiB each): H2D from pageable '
+                                             f'memory + the scan kernel + status read-back, median of 3 wall times')
+            wb.close()
         # end to end on text: LicenseFile#license over byte strings through batch.BatchDetector's
         # two-stage pipeline (host threads prepare batch k + 1 while batch k is on the device:
         # upload, Exact, Dice#match + #confidence, download, Detection objects)
         if run.cfg == 2:   # (the vendored corpus: the texts above are config-2 files)
             from licensee_amd.batch import BatchDetector
             from licensee_amd.dice import DiceEngine
-            det = BatchDetector(DiceEngine(device=dev), nthreads=nthreads)
             chunks = [(big[i:i + 4000], None) for i in range(0, len(big), 4000)] * 2
-            for _ in det.detect_stream(chunks[:1]):
-                pass
-            t_h = time.perf_counter()
-            n_det = sum(len(d) for d in det.detect_stream(chunks))
-            extras['end_to_end_text_files_per_s'] = n_det / (time.perf_counter() - t_h)
+            eng = DiceEngine(device=dev)
+            for mode, key in (('device', 'end_to_end_text_files_per_s'),
+                              ('host', 'end_to_end_text_host_wordset_files_per_s')):
+                det = BatchDetector(eng, nthreads=nthreads, wordset_on=mode)
+                for _ in det.detect_stream(chunks[:1]):
+                    pass
+                t_h = time.perf_counter()
+                n_det = sum(len(d) for d in det.detect_stream(chunks))
+                extras[key] = n_det / (time.perf_counter() - t_h)
+                det.close()
             extras['end_to_end_text_note'] = (f'batch.BatchDetector.detect_stream: {len(chunks)} batches of 4000 of '
-                                              f'the texts above, host prep ({nthreads} threads) of batch k + 1 '
-                                              f'overlapping batch k on the GPU (Copyright, Exact, Dice#match + '
-                                              f'#confidence, Detection objects)')
-            det.close()
-            det.engine.scorer.close()
+                                              f'the texts above, the host stage ({nthreads} threads) of batch k + 1 '
+                                              f'overlapping batch k on the GPU; wordset_on=device: host '
+                                              f'content_normalized, the GPU scans the wordsets '
+                                              f'(dice_batch_upload_text) and runs Exact and Dice#match + '
+                                              f'#confidence; host_wordset: the host scans and interns too')
+            eng.scorer.close()
         extras['host_prep_note'] = (f'normalize+intern+Copyright/Exact of synthetic texts: Python 1 thread; '
                                     f'native (csrc/normalize.cpp) {nthreads} threads on 16000 byte strings '
                                     f'(avg {sum(map(len, big)) / len(big) / 1024:.1f} KiB)')

@@ -225,6 +225,38 @@ int dice_batch_exact(dice_batch *batch, const uint64_t *file_field_mask, void *s
 int dice_batch_download_exact(dice_batch *batch, int32_t *exact, void *stream);
 int dice_exact(dice_ctx *ctx, const dice_files *files, const uint64_t *file_field_mask, int32_t *exact);
 
+/* ---- ContentHelper#wordset on the device ----------------------------------------------
+ * The wordset scan (content_helper.rb:108-110: /(?:[\w\/-](?:'s|(?<=s)')?)+/, ASCII \w) and its
+ * interning into the batch's bitset rows, for texts already normalized (content_normalized,
+ * content_helper.rb:153-168; licensee_host.h lh_normalize_files), so the host threads skip the
+ * scan. dice_vocab_setup gives the context its vocabulary words in id order (n_words must equal
+ * the V of dice_create; ASCII, distinct) and up to 64 extra words: the template field words
+ * outside the vocabulary, numbered as licensee_host.h lh_template_field_masks numbers them, which
+ * the scan reports as field-mask bits (what lh_prep_files' field_mask holds) instead of row bits. */
+int dice_vocab_setup(dice_ctx *ctx, int32_t n_words, const char *const *words, int32_t n_extra,
+                     const char *const *extra);
+/* text[0, text_bytes): the batch's normalized texts as bytes (every non-ASCII character one byte
+ * >= 0x80), file i at text[offsets[i], offsets[i] + text_len[i]), offsets 16-byte aligned;
+ * length[i] = content_normalized.length in characters and cc_false_positive[i] as in dice_files.
+ * The device builds each file's row, |W_F| (every distinct word, in the vocabulary or not) and
+ * field mask (dice_batch_exact with file_field_mask = NULL reads them). Synchronizes `stream`.
+ * status[i] (host, [n]) = 1 for a file with more distinct non-vocabulary words than the device
+ * set holds (384); *n_overflow (may be NULL) counts them. Such a file's row is left empty: the
+ * caller prepares it on the host (lh_prep_files) and sends it with dice_batch_set_rows before
+ * scoring. Same entry point of the reference as dice_batch_upload (LicenseFile#wordset). */
+int dice_batch_upload_text(dice_batch *batch, int64_t n_files, const uint8_t *text, int64_t text_bytes,
+                           const int64_t *offsets, const int32_t *text_len, const int32_t *length,
+                           const uint8_t *cc_false_positive, uint8_t *status, int64_t *n_overflow,
+                           void *stream);
+/* Overwrite the rows, |W_F| and field masks (NULL: zero) of files index[0..k) of the resident
+ * batch (bits: [k][dice_words64(V)]); synchronizes `stream`. */
+int dice_batch_set_rows(dice_batch *batch, int64_t k, const int64_t *index, const uint64_t *bits,
+                        const uint32_t *wordset_size, const uint64_t *field_mask, void *stream);
+/* D2H of the resident rows ([n][dice_words64(V)]), |W_F| and field masks (NULL outputs skipped;
+ * the masks are those of the last dice_batch_upload_text / dice_batch_exact); synchronizes. */
+int dice_batch_download_rows(dice_batch *batch, uint64_t *bits, uint32_t *wordset_size, uint64_t *field_mask,
+                             void *stream);
+
 /* Build step (no device needed): generate + compile the corpus-specialized sparse program
  * with hiprtc for gfx950 and store it in the code-object cache; writes the cache path. */
 int dice_precompile(const dice_templates *templates, char *path, int32_t path_cap);

@@ -63,6 +63,19 @@ int lh_prep_files(lh_ctx *ctx, int64_t n, const char *const *data, const int64_t
                   int32_t *length, uint8_t *cc, uint8_t *copyright, int32_t *exact,
                   uint8_t *status, uint64_t *field_mask);
 
+/* Batched content_normalized (content_helper.rb:153-168) for the device wordset scan
+ * (licensee_dice.h dice_batch_upload_text): file i's normalized text as bytes -- every
+ * non-ASCII character one byte 0x80, since the wordset's [\w/-] is ASCII -- at
+ * out[off[i], off[i] + tlen[i]), offsets 16-byte aligned, files placed in completion order in
+ * the caller's `cap` bytes; length[i] = the text's length in characters (len_F), cc /
+ * copyright as lh_prep_files. status[i]: 0 ok; 1 outside the native envelope (the caller
+ * normalizes that file itself, off[i] = -1); 3 no room left in `out` (retry with room).
+ * Returns the bytes of `out` used (-1 on bad arguments). */
+int64_t lh_normalize_files(lh_ctx *ctx, int64_t n, const char *const *data, const int64_t *lens,
+                           const char *const *filenames, int32_t nthreads, char *out, int64_t cap,
+                           int64_t *off, int32_t *tlen, int32_t *length, uint8_t *cc,
+                           uint8_t *copyright, uint8_t *status);
+
 /* Vocabulary packing (csrc/vocab_pack.cpp): local search over word swaps between bins of
  * bin_bits (32: sparse-program (template, dword) instruction pairs; 64: LDS-kernel
  * (template, u64) records), starting from `init` (a permutation of 0..V-1). sig is

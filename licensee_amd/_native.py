@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = (
     'dice_batch_deferred',
     'dice_ctx_match_kernel', 'dice_exact_setup', 'dice_batch_exact', 'dice_batch_download_exact', 'dice_exact',
     'dice_match_confidence', 'dice_batch_match_confidence', 'dice_match_sharded_confidence',
-    'dice_batch_scored_pairs',
+    'dice_batch_scored_pairs', 'dice_vocab_setup', 'dice_batch_upload_text', 'dice_batch_set_rows',
+    'dice_batch_download_rows',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -195,6 +196,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_exact': (ctypes.c_int, [vp, vp, vp]),
         'dice_batch_download_exact': (ctypes.c_int, [vp, vp, vp]),
         'dice_exact': (ctypes.c_int, [vp, ctypes.POINTER(_Files), vp, vp]),
+        'dice_vocab_setup': (ctypes.c_int, [vp, i32, vp, i32, vp]),
+        'dice_batch_upload_text': (ctypes.c_int, [vp, i64, vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(i64), vp]),
+        'dice_batch_set_rows': (ctypes.c_int, [vp, i64, vp, vp, vp, vp, vp]),
+        'dice_batch_download_rows': (ctypes.c_int, [vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -347,6 +352,16 @@ class Scorer:
             raise ValueError('exact tables: wordset_size [T], field_bits [T, words64(V)], field_need [T]')
         _check(load_library().dice_exact_setup(self._ctx, _ptr(ws), _ptr(fb), _ptr(fn)))
 
+    def vocab_setup(self, words, extra=()):
+        """The device wordset scan's tables (``dice_vocab_setup``): the vocabulary words in id
+        order and up to 64 extra words (template field words outside the vocabulary), ASCII."""
+        enc = [w.encode('ascii') for w in words]
+        ext = [w.encode('ascii') for w in extra]
+        wa = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+        ea = (ctypes.c_char_p * max(len(ext), 1))(*ext)
+        _check(load_library().dice_vocab_setup(self._ctx, len(enc), ctypes.cast(wa, ctypes.c_void_p),
+                                               len(ext), ctypes.cast(ea, ctypes.c_void_p)))
+
     def exact(self, files: FileBatch, field_mask: Optional[np.ndarray] = None) -> np.ndarray:
         """Exact#match per file on the device: template index or -1."""
         out = np.empty(files.n, np.int32)
@@ -406,6 +421,46 @@ class DeviceBatch:
                                                     ids.dtype.itemsize, _ptr(wf), _ptr(ln), _ptr(cc),
                                                     stream or None))
         self.n = n
+
+    def upload_text(self, text: np.ndarray, offsets, text_len, length, cc_false_positive, stream: int = 0):
+        """Upload normalized texts (``dice_batch_upload_text``: uint8 ``text``, file i at
+        ``text[offsets[i]:offsets[i] + text_len[i]]``, 16-byte aligned offsets); the device scans
+        the wordsets. Returns the [n] status array (1 = too many distinct words outside the
+        vocabulary for the device set: send that file with :meth:`set_rows`)."""
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        tl = np.ascontiguousarray(text_len, dtype=np.int32)
+        ln = np.ascontiguousarray(length, dtype=np.int32)
+        cc = np.ascontiguousarray(cc_false_positive, dtype=np.uint8)
+        n = off.shape[0]
+        if not (tl.shape == ln.shape == cc.shape == (n,)):
+            raise ValueError('inconsistent text-upload shapes')
+        st = np.zeros(n, np.uint8)
+        nov = ctypes.c_int64(0)
+        _check(load_library().dice_batch_upload_text(self._b, n, _ptr(text), int(text.shape[0]), _ptr(off), _ptr(tl),
+                                                     _ptr(ln), _ptr(cc), _ptr(st), ctypes.byref(nov), stream or None))
+        self.n = n
+        return st
+
+    def set_rows(self, index, bits, wordset_size, field_mask=None, stream: int = 0):
+        """Overwrite rows / |W_F| / field masks of the resident files ``index`` (``dice_batch_set_rows``)."""
+        idx = np.ascontiguousarray(index, dtype=np.int64)
+        b = np.ascontiguousarray(bits, dtype=np.uint64)
+        wf = np.ascontiguousarray(wordset_size, dtype=np.uint32)
+        fm = None if field_mask is None else np.ascontiguousarray(field_mask, dtype=np.uint64)
+        k = idx.shape[0]
+        if b.shape != (k, words64(self.scorer.n_vocab)) or wf.shape != (k,) or (fm is not None and fm.shape != (k,)):
+            raise ValueError('set_rows: index [k], bits [k, words64(V)], wordset_size [k], field_mask [k]')
+        _check(load_library().dice_batch_set_rows(self._b, k, _ptr(idx), _ptr(b), _ptr(wf), _ptr(fm), stream or None))
+
+    def download_rows(self, stream: int = 0):
+        """The resident rows [n, words64(V)], |W_F| [n] and field masks [n] (``dice_batch_download_rows``)."""
+        n = self.n
+        bits = np.empty((n, words64(self.scorer.n_vocab)), np.uint64)
+        wf = np.empty(n, np.uint32)
+        fm = np.empty(n, np.uint64)
+        _check(load_library().dice_batch_download_rows(self._b, _ptr(bits), _ptr(wf), _ptr(fm), stream or None))
+        return bits, wf, fm
 
     def match(self, threshold: float, stream: int = 0, confidence: bool = False):
         lib = load_library()

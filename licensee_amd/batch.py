@@ -4,12 +4,14 @@ The reference evaluates ``[Copyright, Exact, Dice].map(new).find(&:match)`` per 
 (license_file.rb:67-69, project_file.rb:69-80) and falls back to ``License 'other'``
 (license_file.rb:92-98). Here the whole chain runs in bulk:
 
-  host (liblicensee_host.so, threads): decode, normalize, intern, Copyright, the per-file
-                                       mask of non-vocabulary field words
-  GPU  (liblicensee_dice.so):          Exact#match (dice_batch_exact: |W_F| == |W_t| and
+  host (liblicensee_host.so, threads): decode, content_normalized, Copyright, the CC flag
+  GPU  (liblicensee_dice.so):          the wordset scan + vocabulary bitsets + field-word
+                                       masks (dice_batch_upload_text, content_helper.rb:108-110),
+                                       Exact#match (dice_batch_exact: |W_F| == |W_t| and
                                        W_t ⊆ W_F, exact.rb:6-12) and Dice#match / #confidence
                                        on the same resident batch
-(``exact_on='host'`` keeps Exact in the host threads, the round-2 split.)
+(``wordset_on='host'`` scans and interns in the host threads instead, the round-5 split;
+``exact_on='host'`` keeps Exact in the host threads too, the round-2 split.)
 
 Results equal the per-file Python chain (tests/test_gpu_golden.py::test_batch_chain).
 """
@@ -35,18 +37,24 @@ class BatchDetector:
     ``engine`` defaults to the process-wide :func:`dice.default_engine` (the vendored
     corpus); pass a :class:`dice.DiceEngine` to use another corpus or device."""
 
-    def __init__(self, engine=None, nthreads: int = 8, exact_on: str = 'device'):
+    def __init__(self, engine=None, nthreads: int = 8, exact_on: str = 'device', wordset_on: str = 'device'):
         from .dice import default_engine
         from .native_host import HostPrep
         if exact_on not in ('device', 'host'):
             raise ValueError("exact_on is 'device' or 'host'")
+        if wordset_on not in ('device', 'host'):
+            raise ValueError("wordset_on is 'device' or 'host'")
         self.engine = engine if engine is not None else default_engine()
         self.host = HostPrep(self.engine.corpus)
         self.nthreads = nthreads
         self.exact_on = exact_on if self.host.field_need is not None else 'host'
+        # the device scan reports the non-vocabulary field words as mask bits for device Exact
+        self.wordset_on = wordset_on if self.exact_on == 'device' else 'host'
         self._batch = None          # one device batch, reused by every detect() and grown on demand
         if self.exact_on == 'device':
             self.engine.scorer.exact_setup(*exact_tables(self.engine.corpus, self.host))
+        if self.wordset_on == 'device':
+            self.engine.scorer.vocab_setup(self.engine.corpus.vocab, self.host.nv_fields)
 
     def _device_batch(self, n: int):
         if self._batch is None or self._batch.capacity < n:
@@ -86,13 +94,39 @@ class BatchDetector:
 
     def _prep(self, contents, filenames=None):
         """Host stage (liblicensee_host.so threads; ctypes releases the GIL during the call)."""
+        if self.wordset_on == 'device':
+            return ('text', self.host.normalize_files(contents, filenames, nthreads=self.nthreads), contents, filenames)
         field_masks = self.exact_on == 'device'
         fb, copyright, third, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads,
                                                        field_masks=field_masks)
         return fb, copyright, third
 
+    def _score_text(self, prepped, thr):
+        """Device stage of wordset_on='device': upload the normalized texts (the device scans and
+        interns the wordsets), patch the rare files whose distinct non-vocabulary words overflow
+        the device set with host-prepared rows, then Exact + Dice#match/#confidence."""
+        import numpy as np
+        _, (text, off, tl, ln, cc, copyright, _), contents, filenames = prepped
+        n = len(off)
+        b = self._device_batch(max(n, 1))
+        st = b.upload_text(text, off, tl, ln, cc)
+        over = np.nonzero(st)[0]
+        if over.size:
+            sub = [contents[i] for i in over]
+            sfn = [filenames[i] for i in over] if filenames is not None else None
+            fb, _, fm, _ = self.host.prep_files(sub, sfn, nthreads=self.nthreads, field_masks=True)
+            b.set_rows(over, fb.bits, fb.wordset_size, fm)
+        b.exact(None)
+        b.match(float(thr), confidence=True)
+        exact = b.download_exact()
+        best, _, score = b.download_match()
+        return copyright, exact, best, score
+
     def _score(self, prepped, thr) -> List[Detection]:
         """Device stage: Exact (device) + Dice#match/#confidence, then the matcher chain's order."""
+        if prepped[0] == 'text':
+            copyright, exact, best, score = self._score_text(prepped, thr)
+            return self._detections(copyright, exact, best, score)
         fb, copyright, third = prepped
         if self.exact_on == 'device':
             b = self._device_batch(max(fb.n, 1))
@@ -104,6 +138,9 @@ class BatchDetector:
         else:
             exact = third
             best, _, score = self.engine.scorer.match(fb, float(thr), confidence=True)
+        return self._detections(copyright, exact, best, score)
+
+    def _detections(self, copyright, exact, best, score) -> List[Detection]:
         templates = self.engine.templates
         no_license, other = License.find('no-license'), License.find('other')
         # the matcher chain's order per file (Copyright, Exact, Dice, else 'other'), over Python lists

@@ -304,6 +304,45 @@ static int transpose_to(dice_batch* b, const E* d_src, int64_t rows, int64_t col
 }
 
 
+// The per-file scalars and, for the tile-layout kernels, the repack (the rows are in b->d_rows).
+// wf == NULL: |W_F| is already on the device (dice_batch_upload_text) and b->n_long is set.
+int dice::upload_tail(dice_batch* b, int64_t n, const uint32_t* wf, const int32_t* len, const uint8_t* cc,
+                      hipStream_t s) {
+    dice_ctx* c = b->ctx;
+    const int64_t n_tiles = (n + kWave - 1) / kWave;
+    const int64_t npad = n_tiles * kWave;
+    b->fmask_device = wf == nullptr;
+    if (wf) HIP_TRY(hipMemcpyAsync(b->d_wf, wf, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_len, len, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b->d_cc, cc, (size_t)n, hipMemcpyHostToDevice, s));
+    if (npad > n) {
+        HIP_TRY(hipMemsetAsync(b->d_wf + n, 0, (size_t)(npad - n) * 4, s));
+        HIP_TRY(hipMemsetAsync(b->d_len + n, 0, (size_t)(npad - n) * 4, s));
+        HIP_TRY(hipMemsetAsync(b->d_cc + n, 0, (size_t)(npad - n), s));
+    }
+    if (c->kind == 3) {   // the postings kernel reads the row-major bitsets
+        if (!wf) return DICE_OK;
+        b->n_long = 0;
+        if (c->prune)
+            for (int64_t i = 0; i < n; ++i) b->n_long += wf[i] > c->prune_max_lf;
+        return DICE_OK;
+    }
+    return dice::repack(b, s);
+}
+
+// The tile-layout kernels' repack of the batch's row-major bitsets (kinds 0-2).
+int dice::repack(dice_batch* b, hipStream_t s) {
+    dice_ctx* c = b->ctx;
+    if (c->kind == 3 || b->n == 0) return DICE_OK;
+    const int64_t n_tiles = (b->n + kWave - 1) / kWave;
+    const int64_t total = n_tiles * c->wq * kWave;
+    const unsigned grid = (unsigned)((total + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(dice_pack_tiles, dim3(grid), dim3(kBlock), 0, s, b->d_rows, b->n, c->w64, c->wq,
+                       c->kind == 1 ? (const int32_t*)c->d_qperm : nullptr, b->d_tiles, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return DICE_OK;
+}
+
 extern "C" {
 
 int32_t dice_words64(int32_t n_vocab) { return n_vocab <= 0 ? 0 : (n_vocab + 63) / 64; }
@@ -329,6 +368,7 @@ static void ctx_free(dice_ctx* c) {
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
     }
     dice::exact_free(c);
+    dice::words_free(c);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -489,7 +529,8 @@ void dice_batch_destroy(dice_batch* b) {
     }
     void* ptrs[] = {b->d_rows, b->d_tiles, b->d_wf,  b->d_len,    b->d_cc,    b->d_best,  b->d_ov,   b->d_score,
                     b->d_mov,  b->d_mscore, b->d_tki, b->d_tks, b->d_stage, b->d_pdense, b->d_ids, b->d_offs,
-                    b->d_defer, b->d_ndefer, b->d_nscored, b->d_exact, b->d_fmask};
+                    b->d_defer, b->d_ndefer, b->d_nscored, b->d_exact, b->d_fmask, b->d_text, b->d_toff,
+                    b->d_tlen, b->d_wstat, b->d_wcnt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -524,34 +565,6 @@ int64_t dice_batch_bytes_per_file(const dice_batch* b) {
     return (int64_t)b->ctx->wq * 16;
 }
 
-// The per-file scalars and, for the tile-layout kernels, the repack (the rows are in b->d_rows).
-static int upload_tail(dice_batch* b, int64_t n, const uint32_t* wf, const int32_t* len, const uint8_t* cc,
-                       hipStream_t s) {
-    dice_ctx* c = b->ctx;
-    const int64_t n_tiles = (n + kWave - 1) / kWave;
-    const int64_t npad = n_tiles * kWave;
-    HIP_TRY(hipMemcpyAsync(b->d_wf, wf, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(b->d_len, len, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(b->d_cc, cc, (size_t)n, hipMemcpyHostToDevice, s));
-    if (npad > n) {
-        HIP_TRY(hipMemsetAsync(b->d_wf + n, 0, (size_t)(npad - n) * 4, s));
-        HIP_TRY(hipMemsetAsync(b->d_len + n, 0, (size_t)(npad - n) * 4, s));
-        HIP_TRY(hipMemsetAsync(b->d_cc + n, 0, (size_t)(npad - n), s));
-    }
-    if (c->kind == 3) {   // the postings kernel reads the row-major bitsets
-        b->n_long = 0;
-        if (c->prune)
-            for (int64_t i = 0; i < n; ++i) b->n_long += wf[i] > c->prune_max_lf;
-        return DICE_OK;
-    }
-    const int64_t total = n_tiles * c->wq * kWave;
-    const unsigned grid = (unsigned)((total + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(dice_pack_tiles, dim3(grid), dim3(kBlock), 0, s, b->d_rows, n, c->w64, c->wq,
-                       c->kind == 1 ? (const int32_t*)c->d_qperm : nullptr, b->d_tiles, n_tiles);
-    HIP_TRY(hipGetLastError());
-    return DICE_OK;
-}
-
 int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
     if (!b || !f) return fail(DICE_E_ARG, "NULL batch/files");
     dice_ctx* c = b->ctx;
@@ -563,9 +576,10 @@ int dice_batch_upload(dice_batch* b, const dice_files* f, void* stream) {
     const int64_t n = f->n_files;
     b->n = n;
     b->n_long = 0;
+    b->fmask_device = false;
     if (n == 0) return DICE_OK;
     HIP_TRY(hipMemcpyAsync(b->d_rows, f->bits, (size_t)n * c->w64 * 8, hipMemcpyHostToDevice, s));
-    return upload_tail(b, n, f->wordset_size, f->length, f->cc_false_positive, s);
+    return dice::upload_tail(b, n, f->wordset_size, f->length, f->cc_false_positive, s);
 }
 
 }  // extern "C"
@@ -577,6 +591,7 @@ int dice::upload_rows_resident(dice_batch* b, const dice_files* f, hipStream_t s
     DeviceGuard g(b->ctx->device);
     b->n = f->n_files;
     b->n_long = 0;
+    b->fmask_device = false;
     if (b->n == 0) return DICE_OK;
     return upload_tail(b, b->n, f->wordset_size, f->length, f->cc_false_positive, s);
 }
@@ -601,6 +616,7 @@ int dice_batch_upload_ids(dice_batch* b, int64_t n, const int64_t* offsets, cons
     hipStream_t s = pick_stream(c, stream);
     b->n = n;
     b->n_long = 0;
+    b->fmask_device = false;
     if (n == 0) return DICE_OK;
     const size_t need = (size_t)std::max<int64_t>(offsets[n], 1) * (size_t)id_bytes;
     if (need > b->ids_bytes) {
@@ -628,7 +644,7 @@ int dice_batch_upload_ids(dice_batch* b, int64_t n, const int64_t* offsets, cons
         hipLaunchKernelGGL(dice_rows_from_ids<uint32_t>, dim3(grid), dim3(256), lds, s, b->d_offs,
                            (const uint32_t*)b->d_ids, n, c->w64, (uint32_t)c->V, b->d_rows);
     HIP_TRY(hipGetLastError());
-    return upload_tail(b, n, wordset_size, length, cc, s);
+    return dice::upload_tail(b, n, wordset_size, length, cc, s);
 }
 
 }  // extern "C"

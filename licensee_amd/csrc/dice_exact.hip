@@ -163,18 +163,19 @@ int dice_batch_exact(dice_batch* b, const uint64_t* file_field_mask, void* strea
     if (!c->exact_ready) return fail(DICE_E_STATE, "dice_exact_setup was not called");
     dice::Guard g(c->device);
     int rc;
-    if (!b->d_exact && ((rc = dice::dalloc_bytes((void**)&b->d_exact, (size_t)b->capacity * 4)) ||
-                        (rc = dice::dalloc_bytes((void**)&b->d_fmask, (size_t)b->capacity * 8))))
-        return rc;
+    if (!b->d_exact && (rc = dice::dalloc_bytes((void**)&b->d_exact, (size_t)b->capacity * 4))) return rc;
+    if (!b->d_fmask && (rc = dice::dalloc_bytes((void**)&b->d_fmask, (size_t)b->capacity * 8))) return rc;
     if (b->n == 0) return DICE_OK;
     hipStream_t s = dice::stream_of(c, stream);
     if (file_field_mask &&
         hipMemcpyAsync(b->d_fmask, file_field_mask, (size_t)b->n * 8, hipMemcpyHostToDevice, s) != hipSuccess)
         return fail(DICE_E_DEVICE, "field mask upload failed");
+    // dice_batch_upload_text built the masks on the device
+    const bool masks = file_field_mask != nullptr || b->fmask_device;
     const unsigned grid = (unsigned)((b->n + 255) / 256);
     hipLaunchKernelGGL(dice::dice_exact_kernel, dim3(grid), dim3(256), (size_t)c->T * 4, s,
                        (const uint64_t*)b->d_rows, b->n, c->w64, (const uint32_t*)b->d_wf,
-                       file_field_mask ? (const uint64_t*)b->d_fmask : nullptr, (const uint4*)c->d_ex_tbl,
+                       masks ? (const uint64_t*)b->d_fmask : nullptr, (const uint4*)c->d_ex_tbl,
                        (const uint64_t*)c->d_ex_need, (const uint4*)c->d_ex_rec, c->T, b->d_exact);
     return hipGetLastError() == hipSuccess ? DICE_OK : fail(DICE_E_DEVICE, "dice_exact_kernel launch failed");
 }

@@ -107,6 +107,11 @@ struct dice_ctx {
     void *h_small_in = nullptr, *h_small_out = nullptr;
     void *d_ex_tbl = nullptr, *d_ex_need = nullptr, *d_ex_rec = nullptr;
     bool exact_ready = false;
+    // device wordset scan (dice_words.hip): the vocabulary table -- tagged slots, keys, lengths,
+    // word offsets and bytes (for long words' tails)
+    void *d_wslots = nullptr, *d_wkeys = nullptr, *d_wlen = nullptr, *d_woff = nullptr, *d_wtxt = nullptr;
+    uint32_t words_bmask = 0, words_id_bits = 0, words_extra = 0;
+    bool words_ready = false;
 };
 
 namespace dice {
@@ -138,6 +143,13 @@ int download_matrix_to(dice_batch* b, uint32_t* ov, double* score, int32_t* tki,
                        hipMemcpyKind kind);
 // the Exact tables (dice_exact.hip)
 void exact_free(dice_ctx* c);
+// the device wordset tables (dice_words.hip)
+void words_free(dice_ctx* c);
+// dice_batch_upload's tail: per-file scalars (wf == NULL: already on the device, b->n_long set),
+// padding, and the tile repack (dice.hip)
+int upload_tail(dice_batch* b, int64_t n, const uint32_t* wf, const int32_t* len, const uint8_t* cc, hipStream_t s);
+// the tile-layout kernels' repack of b->d_rows (no-op for the postings kernels)
+int repack(dice_batch* b, hipStream_t s);
 }  // namespace dice
 
 struct dice_batch {
@@ -178,6 +190,15 @@ struct dice_batch {
     // Exact matcher (dice_batch_exact, lazily allocated): per-file result, field masks
     int32_t* d_exact = nullptr;
     uint64_t* d_fmask = nullptr;
+    bool fmask_device = false;      // d_fmask holds the last upload's masks (dice_batch_upload_text)
+    // dice_batch_upload_text (dice_words.hip): texts, their offsets and lengths, per-file status,
+    // counters {overflowed files, long files}
+    uint8_t* d_text = nullptr;
+    size_t text_cap = 0;
+    int64_t* d_toff = nullptr;
+    int32_t* d_tlen = nullptr;
+    uint8_t* d_wstat = nullptr;
+    uint32_t* d_wcnt = nullptr;
     // small-call batch: d_wf/d_len/d_cc/d_rows carved from d_in, results from d_out
     void *d_in = nullptr, *d_out = nullptr;
 };

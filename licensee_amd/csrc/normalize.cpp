@@ -1201,6 +1201,62 @@ int64_t lh_normalize(lh_ctx* ctx, const char* data, int64_t len, const char* fil
     return (int64_t)u.size();
 }
 
+// Batched content_normalized for the device wordset scan (liblicensee_dice dice_batch_upload_text):
+// each file's normalized text as bytes, a non-ASCII character as the one byte 0x80 (the wordset's
+// [\w/-] is ASCII, content_helper.rb:109, so any such byte only separates tokens), placed at a
+// 16-byte aligned offset of `out` in completion order (a bump allocator over `cap` bytes).
+int64_t lh_normalize_files(lh_ctx* ctx, int64_t n, const char* const* data, const int64_t* lens,
+                           const char* const* filenames, int32_t nthreads, char* out, int64_t cap, int64_t* off,
+                           int32_t* tlen, int32_t* length, uint8_t* cc, uint8_t* copyright, uint8_t* status) {
+    const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+    if (n < 0 || cap < 0 || (n > 0 && (!data || !lens || !out || !off || !tlen || !length || !cc || !copyright || !status)))
+        return -1;
+    if (nthreads < 1) nthreads = 1;
+    std::atomic<int64_t> next{0}, used{0};
+    auto work = [&]() {
+        for (;;) {
+            const int64_t i = next.fetch_add(16);
+            if (i >= n) break;
+            for (int64_t f = i; f < std::min<int64_t>(n, i + 16); ++f) {
+                FileOut o;
+                prep_one(*c, data[f], lens[f], filenames ? filenames[f] : nullptr, true, o);
+                off[f] = -1;
+                tlen[f] = 0;
+                status[f] = (uint8_t)o.status;
+                if (o.status) continue;
+                const size_t sz = o.ascii ? o.normalized8.size() : o.normalized.size();
+                length[f] = (int32_t)sz;   // characters (one byte per character in `out`)
+                cc[f] = o.cc;
+                copyright[f] = o.copyright;
+                const int64_t need = (int64_t)((sz + 15) & ~(size_t)15);
+                int64_t at = used.load(std::memory_order_relaxed);
+                while (at + need <= cap && !used.compare_exchange_weak(at, at + need, std::memory_order_relaxed)) {
+                }
+                if (at + need > cap || sz > (size_t)INT32_MAX) {
+                    status[f] = 3;   // no room: the caller retries the file with a larger buffer
+                    continue;
+                }
+                char* dst = out + at;
+                if (o.ascii) {
+                    memcpy(dst, o.normalized8.data(), sz);
+                } else {
+                    for (size_t k = 0; k < sz; ++k) {
+                        const char32_t ch = o.normalized[k];
+                        dst[k] = ch < 0x80 ? (char)ch : (char)0x80;
+                    }
+                }
+                off[f] = at;
+                tlen[f] = (int32_t)sz;
+            }
+        }
+#ifdef LH_PASS_TIMING
+        pass_flush();
+#endif
+    };
+    run_workers(nthreads, work);
+    return used.load();
+}
+
 // Batched LicenseFile preparation: decode, normalize, wordset scan, intern to the vocabulary
 // bitset, |W_F|, len_F, CC flag, Copyright and Exact matchers.
 //   status[i]: 0 ok; 1 the caller must use the Python path for file i (its outputs unset).

@@ -42,6 +42,8 @@ def _load():
         l.lh_prep_files.argtypes = [vp, i64, cpp, vp, cpp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
         l.lh_template_field_masks.restype = i32
         l.lh_template_field_masks.argtypes = [vp, vp]
+        l.lh_normalize_files.restype = i64
+        l.lh_normalize_files.argtypes = [vp, i64, cpp, vp, cpp, i32, vp, i64, vp, vp, vp, vp, vp, vp]
         l.lh_set_unicode.restype = ctypes.c_int
         l.lh_set_unicode.argtypes = [vp, i32, vp, vp, i32, vp, vp]
         _lib = l
@@ -218,3 +220,62 @@ class HostPrep:
         if field_masks:
             return FileBatch(bits, wf, ln, cc), cr.astype(bool), fm, fell
         return FileBatch(bits, wf, ln, cc), cr.astype(bool), ex, fell
+
+    def normalize_files(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
+                        nthreads: int = 8):
+        """Batched content_normalized for the device wordset scan (``lh_normalize_files``;
+        ``DeviceBatch.upload_text``). Returns (text uint8 [bytes], offsets [n] int64 (16-byte
+        aligned), text_len [n] int32, length [n] int32, cc [n] uint8, copyright [n] bool, fell [n]
+        bool): file i's normalized text at ``text[offsets[i]:offsets[i] + text_len[i]]``, one byte
+        per character (non-ASCII characters as 0x80: the wordset's ``[\\w/-]`` is ASCII). Files the
+        native path does not cover (``fell``) are normalized by the Python path and appended."""
+        lib = _load()
+        n = len(contents)
+        data, keep = _cstrs(contents)
+        lens = np.array([len(x) for x in keep], np.int64)
+        fns = None
+        if filenames is not None:
+            fns, _kf = _cstrs(filenames)
+        cap = int(lens.sum()) + 16 * n + (1 << 16)
+        buf = np.empty(cap, np.uint8)
+        off = np.full(n, -1, np.int64)
+        tl = np.zeros(n, np.int32)
+        ln = np.zeros(n, np.int32)
+        cc = np.zeros(n, np.uint8)
+        cr = np.zeros(n, np.uint8)
+        st = np.zeros(n, np.uint8)
+        used = lib.lh_normalize_files(self._c, n, data, lens.ctypes.data, fns, nthreads, buf.ctypes.data, cap,
+                                      off.ctypes.data, tl.ctypes.data, ln.ctypes.data, cc.ctypes.data,
+                                      cr.ctypes.data, st.ctypes.data)
+        if used < 0:
+            raise RuntimeError('lh_normalize_files failed')
+        # the rest by Python (no room left: rare expansions; outside the native envelope), appended
+        extra = []
+        for i in np.nonzero(st != 0)[0]:
+            i = int(i)
+            if st[i] == 3:   # normalized natively (flags set) but no room left in the buffer
+                txt = self.normalize(contents[i], filenames[i] if filenames is not None else None)
+                extra.append((i, txt, None))
+                continue
+            from .matchers import Copyright
+            from .project_files import LicenseFile
+            lf = LicenseFile(contents[i], filenames[i] if filenames is not None else 'LICENSE')
+            cn = lf.content_normalized() or ''
+            extra.append((i, cn, (lf.potential_false_positive(), Copyright(lf).match() is not None)))
+        if extra:
+            parts = []
+            at = int(used)
+            for i, txt, flags in extra:
+                b = bytes(c if c < 0x80 else 0x80 for c in (ord(ch) for ch in txt)) if not txt.isascii() else txt.encode()
+                off[i] = at
+                tl[i] = len(b)
+                ln[i] = len(txt)
+                if flags is not None:
+                    cc[i], cr[i] = flags
+                pad = (-len(b)) % 16
+                parts.append(b + b'\0' * pad)
+                at += len(b) + pad
+            tail = np.frombuffer(b''.join(parts), np.uint8)
+            buf = np.concatenate([buf[:used], tail])
+            used = at
+        return buf[:used], off, tl, ln, cc, cr.astype(bool), st == 1

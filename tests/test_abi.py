@@ -32,7 +32,7 @@ def test_host_library_exports_every_declared_symbol():
     lib = native_host._load()
     declared = declared_functions('licensee_host.h', 'lh_')
     assert declared == {'lh_create', 'lh_destroy', 'lh_set_templates', 'lh_set_unicode', 'lh_normalize', 'lh_prep_files',
-                        'lh_vocab_pack', 'lh_template_field_masks'}
+                        'lh_vocab_pack', 'lh_template_field_masks', 'lh_normalize_files'}
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(os.listdir(os.path.join(ROOT, 'include'))) == {'licensee_dice.h', 'licensee_host.h'}
@@ -50,6 +50,15 @@ def test_create_rejects_bad_arguments():
     assert b'invalid' in lib.dice_last_error()
     t = _native._Templates(0, 0, None, None, None, None, None, None)
     assert lib.dice_create(ctypes.byref(t), 0, ctypes.byref(ctx)) == -1
+
+
+def test_device_wordset_calls_reject_bad_arguments():
+    lib = _native.load_library()
+    assert lib.dice_vocab_setup(None, 0, None, 0, None) == -1
+    assert lib.dice_batch_upload_text(None, 0, None, 0, None, None, None, None, None, None, None) == -1
+    assert lib.dice_batch_set_rows(None, 0, None, None, None, None, None) == -1
+    assert lib.dice_batch_download_rows(None, None, None, None, None) == -1
+    assert b'NULL' in lib.dice_last_error()
 
 
 def test_sharded_calls_reject_bad_arguments():

@@ -315,3 +315,30 @@ def test_border_lines_fuzz(hp):
         checked += 1
         assert got == LicenseFile(text, 'LICENSE').content_normalized(), (i, text[:300])
     assert checked > 450
+
+
+def _as_scan_bytes(text):
+    """content_normalized as the device wordset scan reads it: one byte per character,
+    non-ASCII characters as 0x80 (lh_normalize_files)."""
+    return bytes(ord(c) if ord(c) < 0x80 else 0x80 for c in text)
+
+
+def test_normalize_files_matches_python(hp):
+    """lh_normalize_files (the device-wordset host stage): per file the normalized text as scan
+    bytes at a 16-byte aligned offset, its length in characters and the CC / Copyright flags --
+    equal to the Python path and to lh_prep_files, the Python-path files (Final_Sigma) appended."""
+    vend = golden('vendored.json')['templates']
+    texts = [c['normalized'] for t in vend for c in t['cases'].values()][:120]
+    texts += ['Copyright 2020 Foo', 'Attribution-NoDerivatives 4.0', 'café license', '', 'ΣΟΦΙΑ license',
+              'CAFÉ LICENCE 软件', "it's the users' s''s a/b-c work's"]
+    texts += [License.find(k).content_normalized() for k in ('mit', 'gpl-3.0', 'vim', 'postgresql')]
+    data = [t.encode('utf-8') for t in texts]
+    text, off, tl, ln, cc, cr, fell = hp.normalize_files(data, ['LICENSE'] * len(texts), nthreads=3)
+    fb, cr2, _, fell2 = hp.prep_files(data, ['LICENSE'] * len(texts), nthreads=3)
+    assert np.array_equal(fell, fell2) and fell.sum() == 1
+    assert (off % 16 == 0).all() and (off >= 0).all() and (off + tl <= len(text)).all()
+    assert np.array_equal(cr, cr2) and np.array_equal(cc, fb.cc_false_positive) and np.array_equal(ln, fb.length)
+    for i, t in enumerate(texts):
+        cn = LicenseFile(t, 'LICENSE').content_normalized()
+        assert bytes(text[off[i]:off[i] + tl[i]]) == _as_scan_bytes(cn), i
+        assert ln[i] == len(cn), i

@@ -12,5 +12,5 @@ C=licensee_amd/csrc
 POST=${POST_SRC:-$C/dice_post.hip}
 PRUNE=${PRUNE_SRC:-$C/dice_prune.hip}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -I$C "$@" -o licensee_amd/lib/var/$NAME.so \
-  $C/dice.hip $C/dice_lds.hip $POST $PRUNE $C/dice_exact.hip $C/dice_program.cpp $C/dice_shard.cpp -lhiprtc
+  $C/dice.hip $C/dice_lds.hip $POST $PRUNE $C/dice_exact.hip $C/dice_words.hip $C/dice_program.cpp $C/dice_shard.cpp -lhiprtc
 echo licensee_amd/lib/var/$NAME.so
