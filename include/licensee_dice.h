@@ -252,6 +252,10 @@ int dice_batch_upload_text(dice_batch *batch, int64_t n_files, const uint8_t *te
  * batch (bits: [k][dice_words64(V)]); synchronizes `stream`. */
 int dice_batch_set_rows(dice_batch *batch, int64_t k, const int64_t *index, const uint64_t *bits,
                         const uint32_t *wordset_size, const uint64_t *field_mask, void *stream);
+/* Page-locked host memory (hipHostMalloc) for upload buffers -- texts, bitsets -- so their H2D
+ * copies run at the link's rate and overlap the host; free with dice_host_free. */
+int dice_host_alloc(int64_t bytes, void **out);
+void dice_host_free(void *ptr);
 /* D2H of the resident rows ([n][dice_words64(V)]), |W_F| and field masks (NULL outputs skipped;
  * the masks are those of the last dice_batch_upload_text / dice_batch_exact); synchronizes. */
 int dice_batch_download_rows(dice_batch *batch, uint64_t *bits, uint32_t *wordset_size, uint64_t *field_mask,

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     'dice_ctx_match_kernel', 'dice_exact_setup', 'dice_batch_exact', 'dice_batch_download_exact', 'dice_exact',
     'dice_match_confidence', 'dice_batch_match_confidence', 'dice_match_sharded_confidence',
     'dice_batch_scored_pairs', 'dice_vocab_setup', 'dice_batch_upload_text', 'dice_batch_set_rows',
-    'dice_batch_download_rows',
+    'dice_batch_download_rows', 'dice_host_alloc', 'dice_host_free',
 )
 DICE_GATHER_HOST = 0
 DICE_GATHER_DEVICE = 1
@@ -200,6 +200,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         'dice_batch_upload_text': (ctypes.c_int, [vp, i64, vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(i64), vp]),
         'dice_batch_set_rows': (ctypes.c_int, [vp, i64, vp, vp, vp, vp, vp]),
         'dice_batch_download_rows': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        'dice_host_alloc': (ctypes.c_int, [i64, ctypes.POINTER(vp)]),
+        'dice_host_free': (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -372,6 +374,29 @@ class Scorer:
             st = files._struct()
             _check(load_library().dice_exact(self._ctx, ctypes.byref(st), _ptr(fm), _ptr(out)))
         return out
+
+
+class PinnedBuffer:
+    """Page-locked host bytes (``dice_host_alloc``) viewed as a uint8 numpy array."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(load_library().dice_host_alloc(int(nbytes), ctypes.byref(p)))
+        self._p = p
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 1)).from_address(p.value))[:self.nbytes]
+
+    def close(self):
+        if getattr(self, '_p', None):
+            self.array = None
+            load_library().dice_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class DeviceBatch:

@@ -51,6 +51,8 @@ class BatchDetector:
         # the device scan reports the non-vocabulary field words as mask bits for device Exact
         self.wordset_on = wordset_on if self.exact_on == 'device' else 'host'
         self._batch = None          # one device batch, reused by every detect() and grown on demand
+        self._pinned = [None, None]  # page-locked text buffers: batch k uploads from one while k + 1 fills the other
+        self._turn = 0
         if self.exact_on == 'device':
             self.engine.scorer.exact_setup(*exact_tables(self.engine.corpus, self.host))
         if self.wordset_on == 'device':
@@ -68,6 +70,22 @@ class BatchDetector:
         if self._batch is not None:
             self._batch.close()
             self._batch = None
+        for i, p in enumerate(self._pinned):
+            if p is not None:
+                p.close()
+                self._pinned[i] = None
+
+    def _text_buffer(self, nbytes: int):
+        """The next page-locked text buffer (alternating, grown on demand)."""
+        from ._native import PinnedBuffer
+        i = self._turn
+        self._turn ^= 1
+        p = self._pinned[i]
+        if p is None or p.nbytes < nbytes:
+            if p is not None:
+                p.close()
+            p = self._pinned[i] = PinnedBuffer(max(nbytes, 2 * p.nbytes if p is not None else nbytes))
+        return p.array
 
     def detect(self, contents: Sequence[Union[str, bytes]], filenames: Optional[Sequence[str]] = None,
                threshold=None) -> List[Detection]:
@@ -95,7 +113,8 @@ class BatchDetector:
     def _prep(self, contents, filenames=None):
         """Host stage (liblicensee_host.so threads; ctypes releases the GIL during the call)."""
         if self.wordset_on == 'device':
-            return ('text', self.host.normalize_files(contents, filenames, nthreads=self.nthreads), contents, filenames)
+            return ('text', self.host.normalize_files(contents, filenames, nthreads=self.nthreads,
+                                                      out=self._text_buffer), contents, filenames)
         field_masks = self.exact_on == 'device'
         fb, copyright, third, _ = self.host.prep_files(contents, filenames, nthreads=self.nthreads,
                                                        field_masks=field_masks)

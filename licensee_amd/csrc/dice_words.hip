@@ -667,6 +667,20 @@ int dice_batch_set_rows(dice_batch* b, int64_t k, const int64_t* index, const ui
     return dice::repack(b, s);
 }
 
+int dice_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes < 0) return fail(DICE_E_ARG, "invalid host allocation");
+    *out = nullptr;
+    if (hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return fail(DICE_E_NOMEM, "hipHostMalloc failed");
+    }
+    return DICE_OK;
+}
+
+void dice_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int dice_batch_download_rows(dice_batch* b, uint64_t* bits, uint32_t* wordset_size, uint64_t* field_mask, void* stream) {
     if (!b) return fail(DICE_E_ARG, "NULL batch");
     dice_ctx* c = b->ctx;
