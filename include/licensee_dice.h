@@ -241,7 +241,7 @@ int dice_vocab_setup(dice_ctx *ctx, int32_t n_words, const char *const *words, i
  * The device builds each file's row, |W_F| (every distinct word, in the vocabulary or not) and
  * field mask (dice_batch_exact with file_field_mask = NULL reads them). Synchronizes `stream`.
  * status[i] (host, [n]) = 1 for a file with more distinct non-vocabulary words than the device
- * set holds (384); *n_overflow (may be NULL) counts them. Such a file's row is left empty: the
+ * set holds (192); *n_overflow (may be NULL) counts them. Such a file's row is left empty: the
  * caller prepares it on the host (lh_prep_files) and sends it with dice_batch_set_rows before
  * scoring. Same entry point of the reference as dice_batch_upload (LicenseFile#wordset). */
 int dice_batch_upload_text(dice_batch *batch, int64_t n_files, const uint8_t *text, int64_t text_bytes,

@@ -24,6 +24,7 @@
 // goes to the wave's LDS set of distinct words (CAS-claimed slots, full keys, long tokens'
 // bytes compared). |W_F| = row bits + field bits + set size. A file whose set would pass
 // kSetMax distinct non-vocabulary words is flagged; the caller prepares it on the host.
+// LDS ~10 KiB per wave at the vendored vocabulary: four 4-wave workgroups per CU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,9 +41,11 @@ namespace dice {
 constexpr int kWordsWaves = 4;          // waves (files in flight) per workgroup
 constexpr int kChunk = 1024;            // bytes per staged chunk (16 per lane)
 constexpr int kWin = 2 * kChunk;        // the LDS window: two chunks, indexed by position & (kWin - 1)
-constexpr int kSetCap = 512;            // per-wave set of distinct non-vocabulary words (slots)
-constexpr int kSetMax = 384;            // more distinct such words: the file is flagged (host path)
-constexpr int kQCap = 128;              // queued tokens (looked up 64 at a time)
+constexpr int kSetCap = 256;            // per-wave set of distinct non-vocabulary words (slots)
+constexpr int kSetMax = 192;            // more distinct such words: the file is flagged (host path);
+                                        // a lookup pass adds at most 64, so the set never overfills
+constexpr uint32_t kQKeep = 63;         // queued tokens left after a flush (lookups run 64 at a time)
+constexpr int kQCap = kQKeep + 33;      // + one block's tokens (32 runs + the open one)
 constexpr uint64_t kLongMark = 1ull << 63;   // set key of a token longer than 16 bytes
 
 // the hash of a token key: (first 16 bytes, little-endian, zero past the token), length, tail hash
@@ -82,16 +85,6 @@ __device__ __forceinline__ void mask_key(uint32_t len, uint64_t& lo, uint64_t& h
     if (len < 8) lo &= (1ull << (8 * len)) - 1;
     if (len <= 8) hi = 0;
     else if (len < 16) hi &= (1ull << (8 * (len - 8))) - 1;
-}
-// the same key from global memory (tokens whose start left the window, the serial path)
-__device__ inline void global_key(const uint8_t* t, uint32_t len, uint64_t& lo, uint64_t& hi) {
-    lo = hi = 0;
-    const uint32_t m = len < 16 ? len : 16;
-    for (uint32_t i = 0; i < m; ++i) {
-        const uint64_t b = t[i];
-        if (i < 8) lo |= b << (8 * i);
-        else hi |= b << (8 * (i - 8));
-    }
 }
 __device__ inline uint32_t tail_hash(const uint8_t* t, uint32_t len) {
     uint32_t h = 2166136261u;
@@ -156,7 +149,7 @@ __device__ inline bool set_insert(uint64_t* sa, uint64_t* sb, uint32_t* so, uint
         for (uint32_t i = 0; i < len && eq; ++i) eq = x[i] == y[i];
         if (eq) return false;
     }
-    return false;   // unreachable: the set holds at most kSetMax + 64 < kSetCap words
+    return false;   // a full set: reached only by a pass that ends above kSetMax (the file is flagged)
 }
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
@@ -211,18 +204,6 @@ __device__ inline uint32_t lookup_pass(const WaveLds& L, uint32_t nq, const Voca
     asm volatile("" ::: "memory");
     if (act && id < 0) fresh = set_insert(L.sa, L.sb, L.so, h, lo, hi, len, tail, pos, ftext) ? 1u : 0u;
     return wave_sum(fresh);
-}
-
-// the regex's loop from a token start p (content_helper.rb:109): the token's end
-__device__ inline uint32_t word_end(const uint8_t* t, uint32_t p, uint32_t n) {
-    while (p < n && word_byte(t[p])) {
-        const uint32_t ch = t[p++];
-        if (p < n && t[p] == '\'') {
-            if (p + 1 < n && t[p + 1] == 's') p += 2;
-            else if (ch == 's') p += 1;
-        }
-    }
-    return p;
 }
 
 __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
@@ -316,24 +297,41 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                     starts &= ~0ull << r;
                     ends &= r >= 63 ? 0ull : ~0ull << (r + 1);
                 }
-                if (ends & q) {
-                    // serial block (a run followed by an apostrophe): the host scan's order, one
-                    // token at a time, keys from global memory
+                // A run ending at an apostrophe continues the token when an 's' precedes or follows
+                // the apostrophe ('s, s'): such blocks take the regex's order serially (rare:
+                // possessives); a run ending at any other apostrophe ends there, as in the fast path.
+                const uint64_t sm = __ballot(p < nb && ch == 's');
+                if (ends & q & ((sm >> 1) | (sm << 1) | 1ull | (1ull << 63))) {
+                    // the byte at x: from the window for chunks c and c + 1, else from memory (an open
+                    // token's earlier bytes; a re-scan running past the next chunk)
+                    auto byte_at = [&](uint32_t x) -> uint32_t {
+                        return x >= c * kChunk && x < (c + 2) * kChunk ? (uint32_t)L.win[x & (kWin - 1)] : (uint32_t)ft[x];
+                    };
                     auto finish = [&](uint32_t a, uint32_t e) {
-                        if (e < nb && ft[e] == '\'') {
-                            const uint32_t e2 = word_end(ft, a, nb);
-                            if (e2 > e) {
-                                resume = e2;
-                                const uint32_t r = e2 - b0;
+                        if ((q >> (e - b0)) & 1u) {
+                            // the regex's loop from the run end (the run itself holds no apostrophe)
+                            uint32_t x = e, prev = byte_at(e - 1);
+                            for (;;) {
+                                if (x < nb && byte_at(x) == '\'') {
+                                    if (x + 1 < nb && byte_at(x + 1) == 's') x += 2;
+                                    else if (prev == 's') x += 1;
+                                }
+                                if (!(x < nb && word_byte(byte_at(x)))) break;
+                                prev = byte_at(x++);
+                            }
+                            if (x > e) {
+                                resume = x;
+                                const uint32_t r = x - b0;
                                 starts = r >= 64 ? 0ull : starts & (~0ull << r);
                                 ends = r >= 63 ? 0ull : ends & (~0ull << (r + 1));
                             }
-                            e = e2;
+                            e = x;
                         }
-                        uint64_t lo, hi;
-                        global_key(ft + a, e - a, lo, hi);
+                        uint64_t lo = olo, hi = ohi;   // the open token's bytes, read at its start
+                        if (a >= b0) window_key(L.win, a, lo, hi);
+                        mask_key(e - a, lo, hi);
                         push(lane == 0, a, e - a, lo, hi);
-                        flush(kQCap - kWave - 1);
+                        flush(kQKeep);
                     };
                     if (open) {
                         const uint32_t e = b0 + (uint32_t)__builtin_ctzll(ends);
@@ -387,7 +385,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hi >> 32), sl) << 32);
                 }
                 push(ends_here, p, len, lo, hi);
-                flush(kQCap - kWave - 1);   // room for the next block's tokens (at most 33)
+                flush(kQKeep);   // room for the next block's tokens (at most 33)
             }
             if (c + 2 < nchunks) chunk_store(c + 2, nx);   // into the slot of chunk c
         }

@@ -1,0 +1,62 @@
+"""Where the batched LicenseFile#license pipeline (batch.BatchDetector.detect_stream) spends its time.
+
+    python tools/e2e_profile.py [batches] [batch_size] [threads]
+
+Times, on synthetic config-2 texts as bytes: the whole two-stage stream; the host stage alone
+(BatchDetector._prep: lh_normalize_files, or lh_prep_files with wordset_on=host); the device
+stage alone (_score: upload + wordset scan + Exact + Dice#match/#confidence + downloads +
+Detection objects) and, inside it, the Detection objects. One JSON line per wordset mode.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    nb = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    bs = int(sys.argv[2]) if len(sys.argv) > 2 else 4000
+    threads = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    from licensee_amd.batch import BatchDetector
+    from licensee_amd.dice import DiceEngine
+    from licensee_amd.synth import SyntheticCorpus
+    eng = DiceEngine(device=0)
+    syn = SyntheticCorpus(eng.corpus)
+    texts = [syn.text(i)[0].encode('utf-8') for i in range(bs * 2)]
+    chunks = [(texts[(k % 2) * bs:(k % 2 + 1) * bs], None) for k in range(nb)]
+    for mode in ('device', 'host'):
+        det = BatchDetector(eng, nthreads=threads, wordset_on=mode)
+        for _ in det.detect_stream(chunks[:2]):
+            pass
+        t0 = time.perf_counter()
+        n = sum(len(d) for d in det.detect_stream(chunks))
+        stream_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        prepped = [det._prep(*c) for c in chunks[:2]]
+        host_s = (time.perf_counter() - t0) / 2
+        t0 = time.perf_counter()
+        for p in prepped:
+            det._score(p, 98.0)
+        dev_s = (time.perf_counter() - t0) / 2
+        if mode == 'device':
+            t0 = time.perf_counter()
+            r = det._score_text(prepped[0], 98.0)
+            raw_s = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            det._detections(*r)
+            obj_s = time.perf_counter() - t0
+        else:
+            raw_s = obj_s = None
+        print(json.dumps({'wordset_on': mode, 'batch': bs, 'threads': threads,
+                          'stream_files_per_s': n / stream_s, 'host_stage_ms': host_s * 1e3,
+                          'device_stage_ms': dev_s * 1e3,
+                          'device_stage_without_objects_ms': raw_s * 1e3 if raw_s else None,
+                          'detection_objects_ms': obj_s * 1e3 if obj_s else None}), flush=True)
+        det.close()
+
+
+if __name__ == '__main__':
+    main()
