@@ -38,6 +38,11 @@
 
 namespace dice {
 
+// Phase-skip diagnostics (tools/build_variant.sh -DWORDS_DIAG=n; results are wrong): 1 skips the
+// lookups, 2 the token keys and queue, 4 the block scan
+#ifndef WORDS_DIAG
+#define WORDS_DIAG 0
+#endif
 constexpr int kWordsWaves = 4;          // waves (files in flight) per workgroup
 constexpr int kChunk = 1024;            // bytes per staged chunk (16 per lane)
 constexpr int kWin = 2 * kChunk;        // the LDS window: two chunks, indexed by position & (kWin - 1)
@@ -86,36 +91,79 @@ __device__ __forceinline__ void mask_key(uint32_t len, uint64_t& lo, uint64_t& h
     if (len <= 8) hi = 0;
     else if (len < 16) hi &= (1ull << (8 * (len - 8))) - 1;
 }
-__device__ inline uint32_t tail_hash(const uint8_t* t, uint32_t len) {
+// Bytes [a, a + 32) of memory at `base` as 8 little-endian u32, from 9 independent aligned loads
+// (one round trip instead of 32 dependent byte loads; the buffers keep 64 bytes of slack).
+__device__ __forceinline__ void load32(const uint8_t* base, uint64_t a, uint32_t (&x)[8]) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (a & ~3ull));
+    uint32_t r[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r[k] = w[k];
+    const uint32_t sh = (uint32_t)(a & 3u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = __builtin_amdgcn_alignbyte(r[k + 1], r[k], sh);
+}
+// FNV-1a of bytes [16, len) of the token at t
+__device__ inline uint32_t tail_hash(const uint8_t* base, uint64_t pos, uint32_t len) {
     uint32_t h = 2166136261u;
-    for (uint32_t i = 16; i < len; ++i) h = fnv_step(h, t[i]);
+    for (uint32_t i = 16; i < len; i += 32) {
+        uint32_t x[8];
+        load32(base, pos + i, x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (i + 4u * k + b < len) h = fnv_step(h, (x[k] >> (8 * b)) & 0xFFu);
+    }
     return h;
 }
+// bytes [from, len) of the tokens at a (in `ba`) and b (in `bb`) are equal
+__device__ inline bool bytes_equal(const uint8_t* ba, uint64_t a, const uint8_t* bb, uint64_t b, uint32_t from,
+                                   uint32_t len) {
+    for (uint32_t i = from; i < len; i += 32) {
+        uint32_t x[8], y[8];
+        load32(ba, a + i, x);
+        load32(bb, b + i, y);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t at = i + 4u * k;
+            const uint32_t m = at >= len ? 0u : len - at >= 4 ? 0xFFFFFFFFu : (1u << (8 * (len - at))) - 1u;
+            diff |= (x[k] ^ y[k]) & m;
+        }
+        if (diff) return false;
+    }
+    return true;
+}
 
-// vocabulary id of the token (lo, hi, len) at t, or -1
+__device__ __forceinline__ uint32_t pick8(const uint4& a, const uint4& b, int j) {   // (no indexed array)
+    const uint4 q = j < 4 ? a : b;
+    const int k = j & 3;
+    return k < 2 ? (k == 0 ? q.x : q.y) : (k == 2 ? q.z : q.w);
+}
+
+// vocabulary id of the token (lo, hi, len) at text[pos], or -1
 __device__ inline int32_t vocab_find(const VocabDev& v, uint64_t h, uint64_t lo, uint64_t hi, uint32_t len,
-                                     const uint8_t* t) {
+                                     const uint8_t* text, uint64_t pos) {
     const uint32_t idmask = (1u << v.id_bits) - 1u;
     const uint32_t tag = ((uint32_t)(h >> 40)) << v.id_bits;
     for (uint32_t b = (uint32_t)h & v.bmask, probe = 0; probe <= v.bmask; b = (b + 1) & v.bmask, ++probe) {
         const uint4* bk = reinterpret_cast<const uint4*>(v.slots + (size_t)b * 8);
         const uint4 s0 = bk[0], s1 = bk[1];
         const uint32_t s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        bool empty = false;
+        uint32_t hits = 0, empty = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            empty |= s[j] == 0;
-            if (s[j] != 0 && (s[j] & ~idmask) == tag) {
-                const int32_t id = (int32_t)(s[j] & idmask) - 1;
-                const uint4 k = v.keys[id];
-                if (((uint64_t)k.x | ((uint64_t)k.y << 32)) == lo && ((uint64_t)k.z | ((uint64_t)k.w << 32)) == hi &&
-                    v.wmeta[id] == len) {
-                    bool eq = true;
-                    const uint8_t* w = v.wtxt + v.woff[id];
-                    for (uint32_t i = 16; i < len && eq; ++i) eq = w[i] == t[i];
-                    if (eq) return id;
-                }
-            }
+            empty |= (uint32_t)(s[j] == 0) << j;
+            hits |= (uint32_t)(s[j] != 0 && (s[j] & ~idmask) == tag) << j;
+        }
+        while (hits) {   // (almost always one candidate)
+            const int j = __builtin_ctz(hits);
+            hits &= hits - 1;
+            const int32_t id = (int32_t)(pick8(s0, s1, j) & idmask) - 1;
+            const uint4 k = v.keys[id];
+            if (((uint64_t)k.x | ((uint64_t)k.y << 32)) == lo && ((uint64_t)k.z | ((uint64_t)k.w << 32)) == hi &&
+                v.wmeta[id] == len && (len <= 16 || bytes_equal(v.wtxt, v.woff[id], text, pos, 16, len)))
+                return id;
         }
         if (empty) return -1;
     }
@@ -142,12 +190,7 @@ __device__ inline bool set_insert(uint64_t* sa, uint64_t* sb, uint32_t* so, uint
         asm volatile("" ::: "memory");
         if (won) return true;
         if (old != a || sb[slot] != b) continue;
-        if (len <= 16) return false;
-        const uint8_t* x = text + so[slot];
-        const uint8_t* y = text + pos;
-        bool eq = true;
-        for (uint32_t i = 0; i < len && eq; ++i) eq = x[i] == y[i];
-        if (eq) return false;
+        if (len <= 16 || bytes_equal(text, so[slot], text, pos, 0, len)) return false;
     }
     return false;   // a full set: reached only by a pass that ends above kSetMax (the file is flagged)
 }
@@ -195,9 +238,9 @@ __device__ inline uint32_t lookup_pass(const WaveLds& L, uint32_t nq, const Voca
         const uint2 m = L.qmeta[lane];
         pos = m.x;
         len = m.y;
-        tail = len > 16 ? tail_hash(ftext + pos, len) : 0u;
+        tail = len > 16 ? tail_hash(ftext, pos, len) : 0u;
         h = words_mix(lo, hi, len, tail);
-        id = vocab_find(v, h, lo, hi, len, ftext + pos);
+        id = vocab_find(v, h, lo, hi, len, ftext, pos);
         if (id >= 0 && (uint32_t)id < v.V) atomicOr(L.row + (id >> 5), 1u << (id & 31));
         else if (id >= 0) fm |= 1ull << (id - (int32_t)v.V);
     }
@@ -264,7 +307,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
         auto flush = [&](uint32_t keep) {   // look up queued tokens until at most `keep` remain
             while (nq > keep && !over) {
                 asm volatile("" ::: "memory");
-                words += lookup_pass(L, nq, v, ft, fm, lane);
+                if (!(WORDS_DIAG & 1)) words += lookup_pass(L, nq, v, ft, fm, lane);
                 const uint32_t done = nq < 64 ? nq : 64;
                 asm volatile("" ::: "memory");
                 // move the rest to the front
@@ -283,7 +326,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
         for (uint32_t c = 0; c < nchunks && !over; ++c) {
             uint4 nx = make_uint4(0, 0, 0, 0);
             if (c + 2 < nchunks) nx = chunk_load(c + 2);
-            for (uint32_t b0 = c * kChunk; b0 < nb && b0 < (c + 1) * kChunk; b0 += kWave) {
+            for (uint32_t b0 = c * kChunk; b0 < nb && b0 < (c + 1) * kChunk && !(WORDS_DIAG & 4); b0 += kWave) {
                 const uint32_t p = b0 + (uint32_t)lane;
                 const uint32_t ch = p < nb ? L.win[p & (kWin - 1)] : 0u;
                 const uint64_t w = __ballot(p < nb && word_byte(ch));
@@ -369,7 +412,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                 const bool ends_here = st && (rest != 0);
                 uint64_t lo = 0, hi = 0;
                 uint32_t len = 0;
-                if (st) window_key(L.win, p, lo, hi);
+                if (st && !(WORDS_DIAG & 2)) window_key(L.win, p, lo, hi);
                 if (ends_here) {
                     len = (uint32_t)__builtin_ctzll(rest);
                     mask_key(len, lo, hi);
@@ -384,7 +427,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                     ohi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hi, sl)) |
                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hi >> 32), sl) << 32);
                 }
-                push(ends_here, p, len, lo, hi);
+                if (!(WORDS_DIAG & 2)) push(ends_here, p, len, lo, hi);
                 flush(kQKeep);   // room for the next block's tokens (at most 33)
             }
             if (c + 2 < nchunks) chunk_store(c + 2, nx);   // into the slot of chunk c
@@ -544,7 +587,7 @@ int dice_vocab_setup(dice_ctx* c, int32_t n_words, const char* const* words, int
     int rc;
     if ((rc = dice::dalloc_bytes(&c->d_wslots, slots.size() * 4)) || (rc = dice::dalloc_bytes(&c->d_wkeys, keys.size() * 16 + 16)) ||
         (rc = dice::dalloc_bytes(&c->d_wlen, wlen.size() * 4 + 4)) || (rc = dice::dalloc_bytes(&c->d_woff, woff.size() * 4 + 4)) ||
-        (rc = dice::dalloc_bytes(&c->d_wtxt, txt.size())))
+        (rc = dice::dalloc_bytes(&c->d_wtxt, txt.size() + 64)))
         return rc;
     if (hipMemcpy(c->d_wslots, slots.data(), slots.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         (n && hipMemcpy(c->d_wkeys, keys.data(), keys.size() * 16, hipMemcpyHostToDevice) != hipSuccess) ||
@@ -576,7 +619,7 @@ int dice_batch_upload_text(dice_batch* b, int64_t n, const uint8_t* text, int64_
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int rc;
     size_t cap8 = (size_t)b->capacity * 8, cap4 = (size_t)b->capacity * 4, cap1 = (size_t)b->capacity, capc = 8;
-    size_t tneed = (size_t)std::max<int64_t>(text_bytes, 16);
+    size_t tneed = (size_t)text_bytes + 64;   // (load32's slack past the last token)
     if (tneed > b->text_cap) {
         if (hipStreamSynchronize(s) != hipSuccess) return fail(DICE_E_DEVICE, "hipStreamSynchronize failed");
         if ((rc = dice::grow(&b->d_text, b->text_cap, tneed))) return rc;
