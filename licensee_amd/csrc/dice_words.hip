@@ -86,6 +86,15 @@ __device__ __forceinline__ void window_key(const uint8_t* win, uint32_t p, uint6
     lo = (uint64_t)x0 | ((uint64_t)x1 << 32);
     hi = (uint64_t)x2 | ((uint64_t)x3 << 32);
 }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
+// window_key at a wave-uniform position, as scalars
+__device__ __forceinline__ void window_key_u(const uint8_t* win, uint32_t p, uint64_t& lo, uint64_t& hi) {
+    window_key(win, p, lo, hi);
+    lo = rfl64(lo);
+    hi = rfl64(hi);
+}
 __device__ __forceinline__ void mask_key(uint32_t len, uint64_t& lo, uint64_t& hi) {
     if (len < 8) lo &= (1ull << (8 * len)) - 1;
     if (len <= 8) hi = 0;
@@ -270,8 +279,11 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
     L.row = L.so + kSetCap;
 
     for (int64_t f = (int64_t)blockIdx.x * kWordsWaves + wave; f < n; f += (int64_t)gridDim.x * kWordsWaves) {
-        const int64_t fo = off[f];
-        const uint32_t nb = (uint32_t)tlen[f];
+        // (uniform values read from memory go through readfirstlane: the state below that derives
+        // from them -- masks, resume, the open token -- then stays scalar instead of being carried
+        // per lane with exec-masked branches)
+        const int64_t fo = (int64_t)(((uint64_t)rfl((uint32_t)((uint64_t)off[f] >> 32)) << 32) | rfl((uint32_t)off[f]));
+        const uint32_t nb = rfl((uint32_t)tlen[f]);
         const uint8_t* ft = text + fo;
         for (int32_t j = lane; j < 2 * w64; j += kWave) L.row[j] = 0;
         for (int j = lane; j < kSetCap; j += kWave) L.sa[j] = 0;
@@ -348,7 +360,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                     // the byte at x: from the window for chunks c and c + 1, else from memory (an open
                     // token's earlier bytes; a re-scan running past the next chunk)
                     auto byte_at = [&](uint32_t x) -> uint32_t {
-                        return x >= c * kChunk && x < (c + 2) * kChunk ? (uint32_t)L.win[x & (kWin - 1)] : (uint32_t)ft[x];
+                        return rfl(x >= c * kChunk && x < (c + 2) * kChunk ? (uint32_t)L.win[x & (kWin - 1)] : (uint32_t)ft[x]);
                     };
                     auto finish = [&](uint32_t a, uint32_t e) {
                         if ((q >> (e - b0)) & 1u) {
@@ -371,7 +383,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                             e = x;
                         }
                         uint64_t lo = olo, hi = ohi;   // the open token's bytes, read at its start
-                        if (a >= b0) window_key(L.win, a, lo, hi);
+                        if (a >= b0) window_key_u(L.win, a, lo, hi);
                         mask_key(e - a, lo, hi);
                         push(lane == 0, a, e - a, lo, hi);
                         flush(kQKeep);
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                         if (!ends) {
                             open = true;
                             ostart = a;
-                            window_key(L.win, a, olo, ohi);
+                            window_key_u(L.win, a, olo, ohi);
                             break;
                         }
                         const uint32_t e = b0 + (uint32_t)__builtin_ctzll(ends);

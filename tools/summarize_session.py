@@ -70,6 +70,15 @@ def main():
         if 'host_prep_native_files_per_s' in hp:
             fh.write(f"\nHost prep (native, {hp.get('host_prep_note', '')}): "
                      f"{hp['host_prep_native_files_per_s']:.3g} files/s; Python: {hp['host_prep_python_files_per_s']:.3g} files/s\n")
+        rates = [('host stage with the device wordset scan (lh_normalize_files)', 'host_normalize_files_per_s'),
+                 ('device wordset scan (dice_batch_upload_text, H2D included)', 'device_wordset_files_per_s'),
+                 ('end to end, BatchDetector.detect_stream, wordset on the device', 'end_to_end_text_files_per_s'),
+                 ('end to end, wordset on the host', 'end_to_end_text_host_wordset_files_per_s')]
+        if any(k in hp for _, k in rates):
+            fh.write('\n| real-text rate (16 host threads) | files/s |\n|---|---|\n')
+            for name, k in rates:
+                if k in hp:
+                    fh.write(f'| {name} | {hp[k]:.3g} |\n')
     print(f'{tag}: bench launch {bench["roofline"]["launch_ms"] * 1e3:.2f} us, rocprof {avg_ns / 1e3:.2f} us, '
           f'traced step {same["ms_per_step"] * 1e3:.2f} us, frac(rocprof) {frac:.3f}')
 
