@@ -824,6 +824,14 @@ def main():
                 t_h = time.perf_counter()
                 n_det = sum(len(d) for d in det.detect_stream(chunks))
                 extras[key] = n_det / (time.perf_counter() - t_h)
+                # the two stages alone, per 4000-file batch (the stream's bound is the slower one)
+                t_h = time.perf_counter()
+                prepped = [det._prep(*c) for c in chunks[:2]]
+                t_m = time.perf_counter()
+                for p in prepped:
+                    det._score(p, args.threshold)
+                extras[key.replace('_files_per_s', '_stage_ms')] = {
+                    'host': (t_m - t_h) / 2 * 1e3, 'device': (time.perf_counter() - t_m) / 2 * 1e3}
                 det.close()
             extras['end_to_end_text_note'] = (f'batch.BatchDetector.detect_stream: {len(chunks)} batches of 4000 of '
                                               f'the texts above, the host stage ({nthreads} threads) of batch k + 1 '
