@@ -163,12 +163,21 @@ class BatchDetector:
         templates = self.engine.templates
         no_license, other = License.find('no-license'), License.find('other')
         # the matcher chain's order per file (Copyright, Exact, Dice, else 'other'), over Python lists
-        # (numpy scalar indexing per file cost as much as the host preparation of the next batch)
-        return [Detection(no_license, 'copyright', 100) if c else
-                Detection(templates[e], 'exact', 100) if e >= 0 else
-                Detection(templates[bi], 'dice', sc) if bi >= 0 else
-                Detection(other, None, None)
-                for c, e, bi, sc in zip(copyright.tolist(), exact.tolist(), best.tolist(), score.tolist())]
+        # (numpy scalar indexing per file cost as much as the host preparation of the next batch);
+        # the cyclic collector paused while the batch's objects are made (they hold no cycles, and
+        # in a process with a large heap its passes cost more than the objects themselves)
+        import gc
+        paused = gc.isenabled()
+        gc.disable()
+        try:
+            return [Detection(no_license, 'copyright', 100) if c else
+                    Detection(templates[e], 'exact', 100) if e >= 0 else
+                    Detection(templates[bi], 'dice', sc) if bi >= 0 else
+                    Detection(other, None, None)
+                    for c, e, bi, sc in zip(copyright.tolist(), exact.tolist(), best.tolist(), score.tolist())]
+        finally:
+            if paused:
+                gc.enable()
 
 
 def exact_tables(corpus, host):

@@ -20,6 +20,19 @@ def main():
     nb = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     bs = int(sys.argv[2]) if len(sys.argv) > 2 else 4000
     threads = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    # (diagnostics: the conditions of bench.py's process) torch initialised with CPU tensor work
+    # done, and/or a large resident heap
+    keep = []
+    if 'torch' in sys.argv[4:]:
+        import torch
+        torch.cuda.init()
+        x = torch.randn(4096, 4096)
+        keep.append((x @ x).sum().item())
+        keep.append(torch.empty(1 << 24, dtype=torch.uint8).pin_memory())
+    if 'heap' in sys.argv[4:]:
+        import numpy as np
+        keep.append(np.ones(1 << 31, np.uint8))
+        keep.append([str(i) for i in range(5_000_000)])
     from licensee_amd.batch import BatchDetector
     from licensee_amd.dice import DiceEngine
     from licensee_amd.synth import SyntheticCorpus
