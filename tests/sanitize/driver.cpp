@@ -112,6 +112,22 @@ int main(int argc, char** argv) {
         lh_prep_files(ctx, n, data.data(), lens.data(), nullptr, 4, bits.data(), wf.data(), length.data(), cc.data(),
                       cr.data(), nullptr, st.data(), fmask.data()))
         return 6;
+    // the device-wordset host stage: normalized texts into a caller buffer, once with room for all and
+    // once with room for about half (the rest report "no room", status 3)
+    {
+        int64_t total = 0;
+        for (int64_t l : lens) total += l;
+        std::vector<int64_t> off(n);
+        std::vector<int32_t> tl(n), ln(n);
+        for (int64_t cap : {total + 16 * n + 65536, total / 2}) {
+            std::vector<char> buf((size_t)std::max<int64_t>(cap, 1));
+            const int64_t used = lh_normalize_files(ctx, n, data.data(), lens.data(), nullptr, 4, buf.data(), cap,
+                                                    off.data(), tl.data(), ln.data(), cc.data(), cr.data(), st.data());
+            if (used < 0 || used > cap) return 9;
+            for (int64_t i = 0; i < n; ++i)
+                if (st[i] == 0 && (off[i] < 0 || off[i] % 16 || off[i] + tl[i] > used)) return 9;
+        }
+    }
     int64_t native = 0, total_len = 0;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t m = lh_normalize(ctx, data[i], lens[i], "LICENSE", 1, nullptr, 0);

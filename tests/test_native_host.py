@@ -342,3 +342,17 @@ def test_normalize_files_matches_python(hp):
         cn = LicenseFile(t, 'LICENSE').content_normalized()
         assert bytes(text[off[i]:off[i] + tl[i]]) == _as_scan_bytes(cn), i
         assert ln[i] == len(cn), i
+
+
+def test_normalize_files_without_room_appends_the_rest(hp):
+    """normalize_files with a buffer too small for every text: the files lh_normalize_files had no room
+    for (status 3) are appended by the wrapper, at 16-byte aligned offsets, with the same bytes."""
+    texts = [License.find(k).content_normalized().encode() for k in ('mit', 'gpl-3.0', 'apache-2.0', 'isc', 'bsd-2-clause')]
+    full = hp.normalize_files(texts, None, nthreads=2)
+    small = hp.normalize_files(texts, None, nthreads=2, out=lambda nbytes: np.empty(20000, np.uint8))
+    for a, b in zip(full[3:6], small[3:6]):
+        assert np.array_equal(a, b)
+    text, off, tl = small[0], small[1], small[2]
+    assert (off % 16 == 0).all() and (off + tl <= len(text)).all()
+    for i in range(len(texts)):
+        assert bytes(text[off[i]:off[i] + tl[i]]) == bytes(full[0][full[1][i]:full[1][i] + full[2][i]])

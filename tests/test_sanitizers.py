@@ -4,7 +4,7 @@ tests/sanitize/driver.cpp links csrc/rx.cpp, normalize.cpp and vocab_pack.cpp bu
 -fsanitize=address,undefined (no recovery), once for baseline x86-64 (the scalar scans) and once
 for x86-64-v3 (the AVX2 scans of csrc/scan.h, as the shipped library is built), and drives every entry point of
 include/licensee_host.h -- lh_create, lh_set_unicode, lh_set_templates, threaded
-lh_prep_files, lh_normalize, lh_vocab_pack, lh_destroy -- over the reference fixture texts
+lh_prep_files, lh_normalize_files (room for all, then for half), lh_normalize, lh_vocab_pack, lh_destroy -- over the reference fixture texts
 (goldens), all 47 template texts, seeded fuzz texts (markup, non-ASCII, contextual
 characters) and long mixed files. Host code only: GPU sanitizers are not available.
 """
