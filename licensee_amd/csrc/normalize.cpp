@@ -983,10 +983,12 @@ bool all_ascii(const char* data, size_t len) {
 // ASCII rule; decoding is the identity)
 void prep_ascii(const Ctx& c, const char* data, int64_t len, bool is_file, FileOut& o) {
     Str8 content;
-    if (is_file) {   // universal newline (project_file.rb:41)
+    const char* cr = is_file ? (const char*)memchr(data, '\r', (size_t)len) : nullptr;
+    if (cr) {   // universal newline (project_file.rb:41); the bytes before the first CR as one copy
         content.resize((size_t)len);
-        size_t w = 0;
-        for (size_t i = 0; i < (size_t)len; ++i) {
+        size_t w = (size_t)(cr - data);
+        memcpy(&content[0], data, w);
+        for (size_t i = w; i < (size_t)len; ++i) {
             if (data[i] == '\r') {
                 content[w++] = '\n';
                 if (i + 1 < (size_t)len && data[i + 1] == '\n') ++i;
@@ -1003,7 +1005,7 @@ void prep_ascii(const Ctx& c, const char* data, int64_t len, bool is_file, FileO
     PASS("cc_flag", o.cc = c.R("cc_false_positive").search(stripped, 0, caps));
     PASS("copyright_matcher", o.copyright = c.R("copyright_match").search(stripped, 0, caps));
     Normalizer<Str8> nz{c, Str8()};
-    o.normalized8 = nz.run(content);
+    PASS("=normalizer_run", o.normalized8 = nz.run(content));
     o.ascii = true;
 }
 
@@ -1219,7 +1221,7 @@ int64_t lh_normalize_files(lh_ctx* ctx, int64_t n, const char* const* data, cons
             if (i >= n) break;
             for (int64_t f = i; f < std::min<int64_t>(n, i + 16); ++f) {
                 FileOut o;
-                prep_one(*c, data[f], lens[f], filenames ? filenames[f] : nullptr, true, o);
+                PASS("=prep_one", prep_one(*c, data[f], lens[f], filenames ? filenames[f] : nullptr, true, o));
                 off[f] = -1;
                 tlen[f] = 0;
                 status[f] = (uint8_t)o.status;

@@ -1,10 +1,11 @@
 """Per-pass timing of the native host preparation (csrc/normalize.cpp built with -DLH_PASS_TIMING).
 
-    python tools/host_prep_passes.py [n_texts] [threads]
+    python tools/host_prep_passes.py [n_texts] [threads] [prep|normalize]
 
 Builds a diagnostic copy of liblicensee_host.so under /tmp, points licensee_amd.native_host at
 it, prepares n synthetic config-2 texts (SyntheticCorpus.text, ~9 KB each, as UTF-8 bytes) and prints the
-seconds spent in every pass (summed over threads) and the batch rate.
+seconds spent in every pass (summed over threads) and the batch rate: lh_prep_files (the whole host
+path, default) or lh_normalize_files (the host stage when the GPU scans the wordsets).
 """
 import os
 import subprocess
@@ -18,6 +19,7 @@ sys.path.insert(0, ROOT)
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     threads = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    mode = sys.argv[3] if len(sys.argv) > 3 else 'prep'
     march = os.environ.get('LH_MARCH', 'x86-64-v3')
     csrc = os.path.join(ROOT, 'licensee_amd', 'csrc')
     so = '/tmp/liblicensee_host_timing.so'
@@ -36,12 +38,14 @@ def main():
     syn = SyntheticCorpus(corpus)
     texts = [syn.text(i)[0].encode('utf-8') for i in range(n)]   # file contents as bytes, as bench.py
     hp = native_host.HostPrep(corpus)
-    hp.prep_files(texts[:50], None, nthreads=threads)
+    run = (lambda t: hp.prep_files(t, None, nthreads=threads)) if mode == 'prep' else \
+        (lambda t: hp.normalize_files(t, None, nthreads=threads))
+    run(texts[:50])
     best = None
     for _ in range(3):   # the best of 3 runs (shared machines are noisy)
         lib.lh_pass_timing(None, 0)
         t0 = time.perf_counter()
-        hp.prep_files(texts, None, nthreads=threads)
+        run(texts)
         wall = time.perf_counter() - t0
         buf = ctypes.create_string_buffer(1 << 16)
         lib.lh_pass_timing(buf, 1 << 16)
@@ -49,8 +53,8 @@ def main():
             best = (wall, buf.value.decode())
     wall = best[0]
     rows = [(l.split()[0], float(l.split()[1])) for l in best[1].splitlines()]
-    tot = sum(s for _, s in rows)
-    print(f'{n} texts ({sum(map(len, texts)) / n / 1024:.1f} KiB avg), {threads} threads: {wall:.3f} s wall, '
+    tot = sum(s for k, s in rows if not k.startswith('='))   # ('=' rows enclose other passes)
+    print(f'{mode}: {n} texts ({sum(map(len, texts)) / n / 1024:.1f} KiB avg), {threads} threads: {wall:.3f} s wall, '
           f'{n / wall:.0f} files/s; passes sum {tot:.3f} s')
     for name, sec in sorted(rows, key=lambda r: -r[1]):
         print(f'  {name:20s} {sec:8.4f} s  {100 * sec / tot:5.1f}%  {sec / n * 1e6:8.1f} us/file')
