@@ -401,6 +401,11 @@ struct WordSet {
     }
 };
 
+#ifndef LH_TEDDY_BYTES
+#define LH_TEDDY_BYTES 4
+#endif
+constexpr int kTeddyBytes = LH_TEDDY_BYTES;   // key bytes in the spelling prefix fingerprint
+
 struct Ctx {
     std::map<std::string, Regex> re;
     std::vector<std::pair<Str, Str>> spell;
@@ -412,10 +417,10 @@ struct Ctx {
     std::vector<int32_t> spell_trie;
     std::vector<int32_t> spell_key;
     uint64_t spell_tok[(1u << 15) / 64] = {};   // spell_tok_slot of every key's first \w run
-    // byte path: the keys' first three bytes as a nibble fingerprint (spell_prefix_mask): 8
+    // byte path: the keys' first four bytes as a nibble fingerprint (spell_prefix_mask): 8
     // buckets; teddy[k][0|1][nibble] = the buckets with a key whose byte k has that low | high
     // nibble (16 entries repeated for both 128-bit lanes)
-    alignas(32) uint8_t teddy[3][2][32] = {};
+    alignas(32) uint8_t teddy[kTeddyBytes][2][32] = {};
     bool teddy_ok = true;
     // Unicode tables (lh_set_unicode): Python str.lower() of non-ASCII code points
     bool unicode = false;
@@ -591,11 +596,11 @@ struct Normalizer {
         clean = false;
     }
 #if defined(__AVX2__)
-    // Bit j: some key could start at q[j] -- its first three bytes pass the nibble fingerprint
-    // (no false negatives; q[j + 1], q[j + 2] past the text read as 0, which no key holds).
+    // Bit j: some key could start at q[j] -- its first four bytes pass the nibble fingerprint
+    // (no false negatives; bytes past the text read as 0, which no key holds).
     uint64_t spell_prefix_mask(const char* q, size_t avail) const {
         alignas(32) char pad[96];
-        if (avail < 66) {
+        if (avail < 64 + kTeddyBytes - 1) {
             memset(pad, 0, sizeof pad);
             memcpy(pad, q, avail);
             q = pad;
@@ -604,7 +609,7 @@ struct Normalizer {
         uint64_t m = 0;
         for (int h = 0; h < 64; h += 32) {
             __m256i r = _mm256_set1_epi8(-1);
-            for (int k = 0; k < 3; ++k) {
+            for (int k = 0; k < kTeddyBytes; ++k) {
                 const __m256i x = _mm256_loadu_si256((const __m256i*)(q + h + k));
                 const __m256i lo = _mm256_shuffle_epi8(_mm256_load_si256((const __m256i*)c.teddy[k][0]), _mm256_and_si256(x, nib));
                 const __m256i hi = _mm256_shuffle_epi8(_mm256_load_si256((const __m256i*)c.teddy[k][1]),
@@ -1068,17 +1073,17 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
             }
         }
         if (nsym > kSpellSyms) throw std::runtime_error("spelling keys: alphabet too large");
-        {   // the byte path's prefix fingerprint: distinct 3-byte prefixes, sorted, in 8 runs
+        {   // the byte path's prefix fingerprint: distinct kTeddyBytes-byte prefixes, sorted, in 8 runs
             std::vector<Str> pre;
             for (const auto& kv : c->spell) {
-                if (kv.first.size() < 3) c->teddy_ok = false;
-                else pre.push_back(kv.first.substr(0, 3));
+                if (kv.first.size() < (size_t)kTeddyBytes) c->teddy_ok = false;
+                else pre.push_back(kv.first.substr(0, kTeddyBytes));
             }
             std::sort(pre.begin(), pre.end());
             pre.erase(std::unique(pre.begin(), pre.end()), pre.end());
             for (size_t j = 0; j < pre.size(); ++j) {
                 const uint8_t bit = (uint8_t)(1u << (j * 8 / pre.size()));
-                for (int k = 0; k < 3; ++k) {
+                for (int k = 0; k < kTeddyBytes; ++k) {
                     const uint32_t ch = (uint32_t)pre[j][(size_t)k];   // ASCII (checked above)
                     for (int lane = 0; lane < 32; lane += 16) {
                         c->teddy[k][0][lane + (ch & 15)] |= bit;
