@@ -155,7 +155,7 @@ bool safe_nonascii(char32_t c) {
 // character whose Python semantics are not a per-character table lookup: the letters re.I
 // equates with ASCII ones (U+0130 İ, U+0131 ı, U+017F ſ, U+212A Kelvin K; U+0130 also lowers
 // to two characters) and U+03A3 Σ (str.lower() applies the Final_Sigma context rule).
-bool python_only(char32_t c) { return c == 0x130 || c == 0x131 || c == 0x17F || c == 0x212A || c == 0x3A3; }
+bool python_only(char32_t c) { return (c == 0x130) | (c == 0x131) | (c == 0x17F) | (c == 0x212A) | (c == 0x3A3); }
 
 // Word keys for the wordset scan (content_helper.rb:109). Tokens are ASCII ([\w/-] with ASCII
 // \w, and apostrophes), so a token's first 16 characters pack into two 64-bit words (one byte
@@ -425,6 +425,10 @@ struct Ctx {
     // Unicode tables (lh_set_unicode): Python str.lower() of non-ASCII code points
     bool unicode = false;
     std::unordered_map<char32_t, char32_t> lower;
+    std::vector<uint64_t> lower_bmp;   // BMP code points with an entry in `lower` (8 KiB)
+    bool has_lower(char32_t ch) const {
+        return ch >= 0x10000 || ((lower_bmp[ch >> 6] >> (ch & 63)) & 1);
+    }
     VocabTable vocab;
     int32_t n_vocab = 0, w64 = 0;
     // templates (Exact)
@@ -562,8 +566,14 @@ struct Normalizer {
             uint64_t starts = w & ~((w << 1) | prev_word);
             prev_word = w >> 63;
 #if defined(__AVX2__)
-            if constexpr (sizeof(C) == 1)
+            if constexpr (sizeof(C) == 1) {
                 if (c.teddy_ok && starts) starts &= spell_prefix_mask(p + b0, n - b0);
+            } else if (c.teddy_ok && starts) {   // the characters narrowed to bytes (non-ASCII: 0xFF, in no key)
+                alignas(32) char nar[64 + kTeddyBytes];
+                const size_t m = std::min<size_t>(64 + kTeddyBytes - 1, n - b0);
+                for (size_t j = 0; j < m; ++j) nar[j] = p[b0 + j] < 128 ? (char)p[b0 + j] : (char)0xFF;
+                starts &= spell_prefix_mask(nar, m);
+            }
 #endif
             while (starts) {
                 const size_t off = (size_t)__builtin_ctzll(starts);
@@ -657,7 +667,10 @@ struct Normalizer {
         const __m256i amp = _mm256_set1_epi32('&'), c127 = _mm256_set1_epi32(127);
         for (; i + 8 <= n; i += 8) {
             __m256i v = _mm256_loadu_si256((const __m256i*)(p + i));
-            if (scan::lanes(_mm256_cmpgt_epi32(v, c127))) break;
+            if (scan::lanes(_mm256_cmpgt_epi32(v, c127))) {   // a block with non-ASCII: one at a time
+                for (size_t k = i; k < i + 8; ++k) downcase_one(cur[k], amps);
+                continue;
+            }
             const __m256i up = _mm256_and_si256(_mm256_cmpgt_epi32(v, A1), _mm256_cmpgt_epi32(Z1, v));
             v = _mm256_add_epi32(v, _mm256_and_si256(up, c32));
             v = _mm256_blendv_epi8(v, sq, _mm256_or_si256(_mm256_cmpeq_epi32(v, dq), _mm256_cmpeq_epi32(v, bt)));
@@ -668,6 +681,22 @@ struct Normalizer {
 #endif
         (void)amps;
         ascii_done_ = i;
+    }
+
+    // one character of the downcase/quote pass (content_helper.rb:34-41; Python str.lower())
+    void downcase_one(C& ch, size_t& amps) const {
+        if (cp(ch) < 128) {
+            if (ch >= 'A' && ch <= 'Z') ch += 32;
+            else if (ch == '"' || ch == '`') ch = '\'';
+            else if (ch == '&') ++amps;
+        } else if constexpr (sizeof(C) == 4) {
+            if (ch == 0x2018 || ch == 0x2019 || ch == 0x201C || ch == 0x201D) {
+                ch = '\'';
+            } else if (c.unicode && c.has_lower(ch)) {
+                auto it = c.lower.find(ch);
+                if (it != c.lower.end()) ch = it->second;
+            }
+        }
     }
 
     // border_markup ^[*-](.*?)[*-]$ -> \1 (content_helper.rb:17, :98): '.' stops at '\n' and '$' holds
@@ -729,21 +758,7 @@ struct Normalizer {
         PASS("downcase_amp_quote", {
             size_t amps = 0;
             downcase_quote_ascii(amps);
-            for (size_t i = ascii_done_; i < cur.size(); ++i) {
-                C& ch = cur[i];
-                if (cp(ch) < 128) {
-                    if (ch >= 'A' && ch <= 'Z') ch += 32;
-                    else if (ch == '"' || ch == '`') ch = '\'';
-                    else if (ch == '&') ++amps;
-                } else if constexpr (sizeof(C) == 4) {
-                    if (ch == 0x2018 || ch == 0x2019 || ch == 0x201C || ch == 0x201D) {
-                        ch = '\'';
-                    } else if (c.unicode) {
-                        auto it = c.lower.find(ch);
-                        if (it != c.lower.end()) ch = it->second;
-                    }
-                }
-            }
+            for (size_t i = ascii_done_; i < cur.size(); ++i) downcase_one(cur[i], amps);
             if (amps) {
                 S out;
                 out.reserve(cur.size() + 2 * amps);
@@ -1035,14 +1050,25 @@ void prep_one_impl(const Ctx& c, const char* data, int64_t len, const char* file
         }
         content.resize(w);
     }
-    for (char32_t ch : content)
-        if (ch >= 0x80 && (c.unicode ? python_only(ch) : !safe_nonascii(ch))) { o.status = 1; return; }
+    bool outside = false;
+    PASS("=u_check", {
+        if (c.unicode) {   // (no early exit: the loop vectorizes)
+            uint32_t any = 0;
+            for (char32_t ch : content) any |= (uint32_t)python_only(ch);
+            outside = any != 0;
+        } else {
+            for (char32_t ch : content)
+                if (ch >= 0x80 && !safe_nonascii(ch)) { outside = true; break; }
+        }
+    });
+    if (outside) { o.status = 1; return; }
     std::vector<long> caps;
-    const Str stripped = ruby_strip(content);
+    Str stripped;
+    PASS("=u_strip", stripped = ruby_strip(content));
     PASS("cc_flag", o.cc = c.R("cc_false_positive").search(stripped, 0, caps));
     PASS("copyright_matcher", o.copyright = c.R("copyright_match").search(stripped, 0, caps));
     Normalizer<Str> nz{c, Str()};
-    o.normalized = nz.run(content);
+    PASS("=u_normalizer_run", o.normalized = nz.run(content));
 }
 
 }  // namespace
@@ -1188,7 +1214,11 @@ int lh_set_unicode(lh_ctx* ctx, int32_t n_lower, const uint32_t* lower_from, con
     for (int32_t i = 1; i < n_word; ++i)
         if (word_lo[i] <= word_hi[i - 1] || word_lo[i] > word_hi[i]) return -1;
     c->lower.clear();
-    for (int32_t i = 0; i < n_lower; ++i) c->lower.emplace(lower_from[i], lower_to[i]);
+    c->lower_bmp.assign(0x10000 / 64, 0);
+    for (int32_t i = 0; i < n_lower; ++i) {
+        c->lower.emplace(lower_from[i], lower_to[i]);
+        if (lower_from[i] < 0x10000) c->lower_bmp[lower_from[i] >> 6] |= 1ull << (lower_from[i] & 63);
+    }
     rx::set_unicode_word_ranges(word_lo, word_hi, n_word);
     c->unicode = true;
     return 0;

@@ -95,14 +95,20 @@ static inline char32_t fold(char32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32
 // Python's \w for \b: [A-Za-z0-9_] plus the non-ASCII code points with str.isalnum() True,
 // installed as sorted inclusive ranges by set_unicode_word_ranges (none: ASCII only).
 static std::vector<std::pair<char32_t, char32_t>> g_word_ranges;
+static std::vector<uint64_t> g_word_bmp;   // the ranges over the BMP as a bitmap (8 KiB)
 
 void set_unicode_word_ranges(const uint32_t* lo, const uint32_t* hi, int32_t n) {
     g_word_ranges.clear();
-    for (int32_t i = 0; i < n; ++i) g_word_ranges.push_back({lo[i], hi[i]});
+    g_word_bmp.assign(0x10000 / 64, 0);
+    for (int32_t i = 0; i < n; ++i) {
+        g_word_ranges.push_back({lo[i], hi[i]});
+        for (uint32_t c = lo[i]; c <= hi[i] && c < 0x10000; ++c) g_word_bmp[c >> 6] |= 1ull << (c & 63);
+    }
 }
 
 bool is_word_char(char32_t c) {
     if (c < 128) return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+    if (c < 0x10000 && !g_word_bmp.empty()) return (g_word_bmp[c >> 6] >> (c & 63)) & 1;
     size_t a = 0, b = g_word_ranges.size();   // first range with hi >= c
     while (a < b) {
         const size_t m = (a + b) / 2;
