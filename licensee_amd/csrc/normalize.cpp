@@ -806,9 +806,11 @@ struct Normalizer {
         PASS("bullet_paren", sub_re(c.R("bullet_paren"), LIT(")(")));
         // STRIP_METHODS (content_helper.rb:89-105)
         PASS("bom", strip_re(c.R("bom")));
+        // (cur is lower case here and re.I's non-ASCII folds to ASCII letters are outside the
+        // native envelope, python_only: a match holds its literal words in lower case)
         PASS("cc_optional", if (contains(cur, LIT("creative commons"))) {
-            strip_re(c.R("cc_dedication"));
-            strip_re(c.R("cc_wiki"));
+            PASS("=cc_dedication", if (contains(cur, LIT("dedication"))) strip_re(c.R("cc_dedication")));
+            PASS("=cc_wiki", if (contains(cur, LIT("creativecommons"))) strip_re(c.R("cc_wiki")));
         });
         PASS("cc0_optional", if (contains(cur, LIT("associating cc0"))) {
             strip_re(c.R("cc_legal_code"));

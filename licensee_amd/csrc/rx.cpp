@@ -651,6 +651,32 @@ static void required_runs(const Node* n, LitRun& cur, LitRun& best) {
     }
 }
 
+// The literal run every match of n begins with: its literals from the start of its mandatory
+// path (zero-width anchors between them skipped) up to the first other node. False once the run
+// has ended.
+static bool leading_run(const Node* n, LitRun& run) {
+    switch (n->kind) {
+        case Node::LIT:
+            if (!run.s.empty() && run.icase != n->icase) return false;
+            run.icase = n->icase;
+            run.s.push_back(n->icase ? fold(n->ch) : n->ch);
+            return true;
+        case Node::SEQ:
+            for (auto& k : n->kids)
+                if (!leading_run(k.get(), run)) return false;
+            return true;
+        case Node::GROUP:
+            return leading_run(n->kids[0].get(), run);
+        case Node::REPEAT:   // the first iteration is mandatory; what follows it may differ
+            if (n->min >= 1) leading_run(n->kids[0].get(), run);
+            return false;
+        case Node::BOL: case Node::EOL: case Node::BOS: case Node::EOS: case Node::WORDB:
+            return true;
+        default:
+            return false;
+    }
+}
+
 // first position >= from where req occurs (ASCII case folded when icase), or npos: candidates
 // by a vector scan for the literal's first and last characters (both cases when folded)
 template <class C>
@@ -709,6 +735,14 @@ Regex::Regex(const std::string& utf8, int flags) {
             req_icase_ = best.icase;
         }
     }
+    {
+        LitRun run;
+        leading_run(root_.get(), run);
+        if (run.s.size() >= 2) {
+            lead_ = run.s;
+            lead_icase_ = run.icase;
+        }
+    }
     // Where a match can start: \A-led patterns only at position 0, ^-led patterns only at line
     // starts (every pattern here is re.M). An alternation qualifies when all its branches do.
     const int lead = lead_anchor(root_.get());
@@ -763,6 +797,10 @@ bool Regex::search_impl(const C* p, size_t n, size_t start, std::vector<long>& c
                 if (pos == n) return false;
                 continue;
             }
+        } else if (!lead_.empty()) {
+            // skip to the next occurrence of the literal every match begins with
+            pos = find_required(p, n, pos, lead_, lead_icase_);
+            if (pos == Str::npos) return false;
         } else if (has_first_) {
             // skip to the next character a match can start with
             if (n_first_list_) {

@@ -87,6 +87,8 @@ private:
     int n_first_list_ = 0;            // (vector scan; 0: use first_)
     Str req_;                         // a literal every match contains (empty: none found)
     bool req_icase_ = false;          // ... compared with ASCII case folding
+    Str lead_;                        // a literal every match begins with (used from 2 characters)
+    bool lead_icase_ = false;
     template <class C>
     bool search_impl(const C* p, size_t n, size_t start, std::vector<long>& caps) const;
     template <class S>
