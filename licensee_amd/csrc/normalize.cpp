@@ -417,6 +417,12 @@ struct Ctx {
     std::vector<int32_t> spell_trie;
     std::vector<int32_t> spell_key;
     uint64_t spell_tok[(1u << 15) / 64] = {};   // spell_tok_slot of every key's first \w run
+    // the keys by that slot (first in union order, then a chain), and each key's first eight
+    // characters packed as bytes with the mask of those it has: a start's run may only match a
+    // key whose slot and first characters it shares (checked before the trie walk)
+    std::vector<int16_t> spell_tok_first = std::vector<int16_t>(1u << 15, -1);
+    std::vector<int16_t> spell_tok_next;
+    std::vector<uint64_t> spell_pre8, spell_pre8_mask;
     // byte path: the keys' first four bytes as a nibble fingerprint (spell_prefix_mask): 8
     // buckets; teddy[k][0|1][nibble] = the buckets with a key whose byte k has that low | high
     // nibble (16 entries repeated for both 128-bit lanes)
@@ -575,6 +581,17 @@ struct Normalizer {
                 starts &= spell_prefix_mask(nar, m);
             }
 #endif
+            // (first, last, length) of every start's run, branch-free: a mask of the starts worth
+            // a trie walk -- few -- instead of a mispredicted branch per start
+            uint64_t hits = 0;
+            for (uint64_t st = starts; st; st &= st - 1) {
+                const unsigned off = (unsigned)__builtin_ctzll(st);
+                const uint64_t rest = ~w >> off;
+                const size_t len = rest ? (size_t)__builtin_ctzll(rest) : 1;
+                const size_t s0 = b0 + off, e = std::min(s0 + len, n) - 1;
+                hits |= (uint64_t)(rest == 0 || spell_tok_hit(cp(p[s0]), cp(p[e]), len)) << off;
+            }
+            starts = hits;   // (a run reaching past the block is checked below)
             while (starts) {
                 const size_t off = (size_t)__builtin_ctzll(starts);
                 starts &= starts - 1;
@@ -590,6 +607,7 @@ struct Normalizer {
                     while (s0 + len < n && word(cp(p[s0 + len]))) ++len;
                 }
                 if (!spell_tok_hit(cp(p[s0]), cp(p[s0 + len - 1]), len)) continue;
+                if (!spell_pre_hit(p, s0, n, spell_tok_slot(cp(p[s0]), cp(p[s0 + len - 1]), len))) continue;
                 size_t klen = 0;
                 const int key = match_at(s0, klen);
                 if (key < 0) continue;
@@ -631,6 +649,21 @@ struct Normalizer {
         return m;
     }
 #endif
+    // some key with this first-run slot has the first (up to) eight characters at p[s0]
+    bool spell_pre_hit(const C* p, size_t s0, size_t n, uint32_t slot) const {
+        uint64_t x = 0;
+        const size_t m = std::min<size_t>(8, n - s0);
+        if constexpr (sizeof(C) == 1) {
+            if (m == 8) memcpy(&x, p + s0, 8);
+            else
+                for (size_t j = 0; j < m; ++j) x |= (uint64_t)(unsigned char)p[s0 + j] << (8 * j);
+        } else {
+            for (size_t j = 0; j < m; ++j) x |= (uint64_t)(p[s0 + j] < 128 ? p[s0 + j] : 0xFF) << (8 * j);
+        }
+        for (int k = c.spell_tok_first[slot]; k >= 0; k = c.spell_tok_next[(size_t)k])
+            if ((x & c.spell_pre8_mask[(size_t)k]) == c.spell_pre8[(size_t)k]) return true;
+        return false;
+    }
     bool spell_tok_hit(char32_t first, char32_t last, size_t len) const {
         const uint32_t h = spell_tok_slot(first, last, len);
         return (c.spell_tok[h >> 6] >> (h & 63)) & 1;
@@ -1101,6 +1134,7 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
             }
         }
         if (nsym > kSpellSyms) throw std::runtime_error("spelling keys: alphabet too large");
+        if (n_spell > 32767) throw std::runtime_error("spelling keys: too many");
         {   // the byte path's prefix fingerprint: distinct kTeddyBytes-byte prefixes, sorted, in 8 runs
             std::vector<Str> pre;
             for (const auto& kv : c->spell) {
@@ -1139,6 +1173,17 @@ lh_ctx* lh_create(int32_t n_patterns, const char* const* names, const char* cons
             while (len < k.size() && kAsciiWord[k[len]]) ++len;
             const uint32_t h = spell_tok_slot(k[0], k[len - 1], len);
             c->spell_tok[h >> 6] |= 1ull << (h & 63);
+            c->spell_tok_next.push_back(-1);   // appended at the chain's end: union order
+            int16_t* link = &c->spell_tok_first[h];
+            while (*link >= 0) link = &c->spell_tok_next[(size_t)*link];
+            *link = (int16_t)i;
+            uint64_t pre = 0, mask = 0;
+            for (size_t j = 0; j < k.size() && j < 8; ++j) {
+                pre |= (uint64_t)(k[j] & 0x7F) << (8 * j);   // (ASCII, checked above)
+                mask |= 0xFFull << (8 * j);
+            }
+            c->spell_pre8.push_back(pre);
+            c->spell_pre8_mask.push_back(mask);
         }
         for (const auto& kv : c->spell) {
             Str8 to;
