@@ -19,14 +19,10 @@
 #include <pthread.h>
 #include <stdint.h>
 #include <string.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
-#include <functional>
 #include <map>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -1003,88 +999,8 @@ constexpr size_t kWorkerMatchDepth = 600000;
 // batch's tail short)
 constexpr int64_t kGrain = 2;
 
-// A persistent pool of batch workers (kWorkerStack stacks, created on first use and kept):
-// spawning threads per call -- fresh stacks to fault in, fresh thread-local tables -- cost a
-// 4,000-file batch more than its own tail. One batch runs on the pool at a time; a concurrent
-// call, or one in a forked child, spawns its own threads instead.
-class WorkerPool {
-public:
-    static WorkerPool& get() {
-        static WorkerPool* p = new WorkerPool();   // (never destroyed: its workers wait until exit)
-        return *p;
-    }
-    // fn on n workers, returning when every one has finished; false: not run (busy, forked, or
-    // no worker could be created)
-    bool run(int32_t n, const std::function<void()>& fn) {
-        if (getpid() != pid_) return false;
-        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-        if (!busy.owns_lock()) return false;
-        std::unique_lock<std::mutex> g(mu_);
-        while ((int32_t)workers_ < n) {
-            pthread_attr_t attr;
-            pthread_attr_init(&attr);
-            pthread_attr_setstacksize(&attr, kWorkerStack);
-            pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
-            auto* a = new Start{this, workers_, gen_};
-            pthread_t id;
-            const int rc = pthread_create(&id, &attr, &WorkerPool::entry, a);
-            pthread_attr_destroy(&attr);
-            if (rc != 0) {
-                delete a;
-                break;
-            }
-            ++workers_;
-        }
-        if (workers_ == 0) return false;
-        want_ = std::min<int32_t>(n, workers_);
-        left_ = want_;
-        job_ = &fn;
-        ++gen_;
-        cv_.notify_all();
-        done_.wait(g, [&] { return left_ == 0; });
-        job_ = nullptr;
-        return true;
-    }
-
-private:
-    struct Start {
-        WorkerPool* pool;
-        int32_t index;
-        uint64_t gen;   // the generation current at creation (the next one is its first job)
-    };
-    WorkerPool() : pid_(getpid()) {}
-    static void* entry(void* p) {
-        Start s = *static_cast<Start*>(p);
-        delete static_cast<Start*>(p);
-        rx::set_match_depth(kWorkerMatchDepth);
-        s.pool->loop(s.index, s.gen);
-        return nullptr;
-    }
-    void loop(int32_t index, uint64_t seen) {
-        std::unique_lock<std::mutex> g(mu_);
-        for (;;) {
-            cv_.wait(g, [&] { return gen_ != seen; });
-            seen = gen_;
-            if (index >= want_) continue;
-            const std::function<void()>* fn = job_;
-            g.unlock();
-            (*fn)();
-            g.lock();
-            if (--left_ == 0) done_.notify_one();
-        }
-    }
-    const pid_t pid_;
-    std::mutex run_mu_, mu_;
-    std::condition_variable cv_, done_;
-    int32_t workers_ = 0, want_ = 0, left_ = 0;
-    uint64_t gen_ = 0;
-    const std::function<void()>* job_ = nullptr;
-};
-
 template <class F>
 void run_workers(int32_t nthreads, F& work) {
-    static const bool no_pool = getenv("LH_NO_POOL") != nullptr;   // (A/B diagnostics: tools/host_scaling.py)
-    if (!no_pool && WorkerPool::get().run(nthreads, std::function<void()>([&] { work(); }))) return;
     struct Arg {
         F* fn;
     } arg{&work};

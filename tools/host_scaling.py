@@ -3,8 +3,9 @@
     python tools/host_scaling.py [max_threads]
 
 Prints files/s for 1, 2, 4, ... max_threads threads on 16,000 synthetic config-2 texts (bytes) in
-batches of 16,000 / 4,000 / 1,000 files. LH_NO_POOL=1 in the environment makes every call spawn
-its own worker threads (the pre-pool behaviour) for an A/B.
+batches of 16,000 / 4,000 / 1,000 files. (Round 6 measured a persistent worker pool against
+threads spawned per call with it: the pool was 5-12% slower at 4-16 threads on the GPU box,
+profiles/raw/r6g_host_scaling_*.txt, and was removed.)
 """
 import os
 import sys
@@ -36,7 +37,7 @@ def main():
                     hp.normalize_files(big[i:i + bs], None, nthreads=th)
                 best = min(best, time.perf_counter() - t0)
             row.append(f'batch {bs}: {len(big) / best:9.3g}')
-        print(f'{"no pool" if os.environ.get("LH_NO_POOL") else "pool"} threads {th:2d}: ' + '  '.join(row), flush=True)
+        print(f'threads {th:2d}: ' + '  '.join(row), flush=True)
         th *= 2
 
 
