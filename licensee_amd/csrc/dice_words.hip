@@ -52,6 +52,11 @@ constexpr int kSetMax = 192;            // more distinct such words: the file is
 constexpr uint32_t kQKeep = 63;         // queued tokens left after a flush (lookups run 64 at a time)
 constexpr int kQCap = kQKeep + 33;      // + one block's tokens (32 runs + the open one)
 constexpr uint64_t kLongMark = 1ull << 63;   // set key of a token longer than 16 bytes
+constexpr uint32_t kFastPos = kQCap * 16 / 2;   // run starts + ends of a fast-path chunk (u16 each in
+                                                // the queue's qlo + qhi area)
+#ifndef WORDS_BLOCKS_ONLY
+#define WORDS_BLOCKS_ONLY 0   // 1: every chunk through the block loop (A/B: tools/build_variant.sh)
+#endif
 
 // the hash of a token key: (first 16 bytes, little-endian, zero past the token), length, tail hash
 __host__ __device__ inline uint64_t words_mix(uint64_t lo, uint64_t hi, uint32_t len, uint32_t tail) {
@@ -232,21 +237,15 @@ struct WaveLds {
     uint32_t* row;     // [2 * w64]
 };
 
-// One lookup pass over the first min(nq, 64) queued tokens (lane = token): the vocabulary bit,
+// One lookup pass over up to 64 tokens (lane = token; `act` lanes hold one): the vocabulary bit,
 // the field-mask bit or the set; returns the number of new set words (wave total).
-__device__ inline uint32_t lookup_pass(const WaveLds& L, uint32_t nq, const VocabDev& v, const uint8_t* ftext,
-                                       uint64_t& fm, int lane) {
+__device__ inline uint32_t lookup_tokens(const WaveLds& L, bool act, uint64_t lo, uint64_t hi, uint32_t len,
+                                         uint32_t pos, const VocabDev& v, const uint8_t* ftext, uint64_t& fm) {
     uint32_t fresh = 0;
-    const bool act = (uint32_t)lane < nq;
-    uint64_t lo = 0, hi = 0, h = 0;
-    uint32_t len = 0, pos = 0, tail = 0;
+    uint64_t h = 0;
+    uint32_t tail = 0;
     int32_t id = -1;
     if (act) {
-        lo = L.qlo[lane];
-        hi = L.qhi[lane];
-        const uint2 m = L.qmeta[lane];
-        pos = m.x;
-        len = m.y;
         tail = len > 16 ? tail_hash(ftext, pos, len) : 0u;
         h = words_mix(lo, hi, len, tail);
         id = vocab_find(v, h, lo, hi, len, ftext, pos);
@@ -256,6 +255,39 @@ __device__ inline uint32_t lookup_pass(const WaveLds& L, uint32_t nq, const Voca
     asm volatile("" ::: "memory");
     if (act && id < 0) fresh = set_insert(L.sa, L.sb, L.so, h, lo, hi, len, tail, pos, ftext) ? 1u : 0u;
     return wave_sum(fresh);
+}
+
+// ... over the first min(nq, 64) queued tokens
+__device__ inline uint32_t lookup_pass(const WaveLds& L, uint32_t nq, const VocabDev& v, const uint8_t* ftext,
+                                       uint64_t& fm, int lane) {
+    const bool act = (uint32_t)lane < nq;
+    uint64_t lo = 0, hi = 0;
+    uint32_t len = 0, pos = 0;
+    if (act) {
+        lo = L.qlo[lane];
+        hi = L.qhi[lane];
+        const uint2 m = L.qmeta[lane];
+        pos = m.x;
+        len = m.y;
+    }
+    return lookup_tokens(L, act, lo, hi, len, pos, v, ftext, fm);
+}
+
+// The classes of four bytes (little-endian in x) as 4-bit masks: [\w/-] (ASCII \w; bytes >= 0x80
+// never match), '\'' and 's'. SWAR on the low seven bits (no carries between bytes), then the
+// bytes with the high bit set are cleared.
+__device__ __forceinline__ void classify4(uint32_t x, uint32_t& w, uint32_t& q, uint32_t& s) {
+    const uint32_t hib = x & 0x80808080u, y = x & 0x7F7F7F7Fu, H = 0x80808080u;
+    auto eq = [&](uint32_t z) { return ~(z + 0x7F7F7F7Fu) & H; };   // per byte: z == 0 (z < 0x80)
+    const uint32_t t = y | 0x20202020u;
+    const uint32_t alpha = (t + 0x1F1F1F1Fu) & ~(t + 0x05050505u) & H;   // 'a' <= t <= 'z'
+    const uint32_t digit = (y + 0x50505050u) & ~(y + 0x46464646u) & H;   // '0' <= y <= '9'
+    const uint32_t under = eq(y ^ 0x5F5F5F5Fu);                           // '_'
+    const uint32_t slash = eq((y | 0x02020202u) ^ 0x2F2F2F2Fu);           // '/' or '-'
+    auto pack = [](uint32_t m) { return ((m >> 7) * 0x10204080u) >> 28; };   // bits 7, 15, 23, 31 -> 0..3
+    w = pack((alpha | digit | under | slash) & ~hib);
+    q = pack(eq(y ^ 0x27272727u) & ~hib);
+    s = pack(eq(y ^ 0x73737373u) & ~hib);
 }
 
 __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
@@ -306,6 +338,7 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
         uint64_t olo = 0, ohi = 0;   // its first 16 bytes (from the window at its start)
         uint32_t resume = 0;         // after a serial block: tokens start at or after it
         uint64_t prevw = 0;
+        uint32_t ptail = 0;          // the last 4 bytes of the previous chunk (fast path)
         auto push = [&](bool has, uint32_t p, uint32_t len, uint64_t lo, uint64_t hi) {
             const uint64_t bal = __ballot(has);
             if (has) {
@@ -338,6 +371,118 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
         for (uint32_t c = 0; c < nchunks && !over; ++c) {
             uint4 nx = make_uint4(0, 0, 0, 0);
             if (c + 2 < nchunks) nx = chunk_load(c + 2);
+            const uint32_t c0 = c * kChunk;
+#if !WORDS_BLOCKS_ONLY
+            // The chunk at once (most chunks): a lane classifies its 16 bytes and the 4 on either
+            // side (SWAR), and the regex's tokens are the runs of [\w/-] joined by the apostrophes
+            // it consumes -- after a word character, one followed by 's' (the 's' then continues
+            // the token) or one preceded by 's'. That rule is exact unless an 's' consumed that
+            // way is itself followed by an apostrophe ("'s'"): such a chunk, one whose last two
+            // bytes hold a joining apostrophe (the block loop of a next chunk must not start inside
+            // the suffix), one a serial re-scan reached into, or one with more than kFastPos run
+            // starts and ends takes the block loop below. The k-th run end closes the k-th run
+            // start (the open token first); tokens are looked up 64 at a time straight from the
+            // window.
+            // (resume == c0: a re-scan consumed the run that reaches the chunk -- its end at c0 is
+            // not a token end: the block loop's resume mask handles it)
+            bool fast = resume == 0 || resume < c0;
+            uint32_t starts = 0, ends = 0, ns = 0, ne = 0, ex = 0, NS = 0, NE = 0, wlast = 0;
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (fast) {
+                const uint32_t base = c0 + 16u * (uint32_t)lane;
+                x = *reinterpret_cast<const uint4*>(L.win + (base & (kWin - 1)));
+                const uint32_t before = lane == 0 ? ptail : *reinterpret_cast<const uint32_t*>(L.win + ((base - 4u) & (kWin - 1)));
+                const uint32_t after = *reinterpret_cast<const uint32_t*>(L.win + ((base + 16u) & (kWin - 1)));
+                // 24 bytes: [base - 4, base + 20), bit j = byte base - 4 + j
+                uint32_t w24 = 0, q24 = 0, s24 = 0;
+                const uint32_t xs[6] = {before, x.x, x.y, x.z, x.w, after};
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    uint32_t a, b, d;
+                    classify4(xs[k], a, b, d);
+                    w24 |= a << (4 * k);
+                    q24 |= b << (4 * k);
+                    s24 |= d << (4 * k);
+                }
+                // bytes outside [0, nb)
+                const int64_t lo_pos = (int64_t)base - 4, hi_pos = (int64_t)base + 20;
+                const uint32_t v_lo = lo_pos >= 0 ? 0u : (uint32_t)(-lo_pos);          // invalid low bytes
+                const uint32_t v_hi = hi_pos <= (int64_t)nb ? 24u : (uint32_t)max<int64_t>((int64_t)nb - lo_pos, 0);
+                const uint32_t vm = (v_hi >= 24 ? 0xFFFFFFu : (1u << v_hi) - 1u) & ~((1u << v_lo) - 1u);
+                w24 &= vm;
+                q24 &= vm;
+                s24 &= vm;
+                const uint32_t join = q24 & (w24 << 1) & ((s24 >> 1) | (s24 << 1));
+                const uint32_t W = w24 | join;
+                const uint32_t tri = q24 & (s24 >> 1) & (q24 >> 2);   // "'s'" starting at bit j
+                const bool hazard = (tri & 0x000FFFFEu) != 0 || (lane == kWave - 1 && (join & (3u << 18)) != 0);
+                const uint32_t wm = (W >> 4) & 0xFFFFu, prev = (W >> 3) & 1u;
+                const uint32_t wp = ((wm << 1) | prev) & 0xFFFFu;
+                starts = wm & ~wp;
+                ends = ~wm & wp & 0xFFFFu;
+                wlast = (uint32_t)__builtin_amdgcn_readlane((int)(wm >> 15), kWave - 1);
+                ns = (uint32_t)__builtin_popcount(starts);
+                ne = (uint32_t)__builtin_popcount(ends);
+                const uint32_t inc = wave_incl_scan(ns | (ne << 16));
+                ex = inc - (ns | (ne << 16));
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+                NS = tot & 0xFFFFu;
+                NE = tot >> 16;
+                const uint32_t o = open ? 1u : 0u;   // (ends pair with the open token, then the starts)
+                fast = __ballot(hazard) == 0 && NS + NE <= kFastPos && NE <= NS + o && NS + o <= NE + 1;
+            }
+            if (fast) {
+                // run starts then run ends, as chunk offsets, in the (empty) queue's key area
+                uint16_t* S = reinterpret_cast<uint16_t*>(L.qlo);
+                uint16_t* E = S + NS;
+                for (uint32_t m = starts, k = ex & 0xFFFFu; m; m &= m - 1, ++k)
+                    S[k] = (uint16_t)(16u * (uint32_t)lane + (uint32_t)__builtin_ctz(m));
+                for (uint32_t m = ends, k = ex >> 16; m; m &= m - 1, ++k)
+                    E[k] = (uint16_t)(16u * (uint32_t)lane + (uint32_t)__builtin_ctz(m));
+                asm volatile("" ::: "memory");
+                const uint32_t o = open ? 1u : 0u;
+                for (uint32_t t0 = 0; t0 < NE && !over; t0 += kWave) {
+                    const uint32_t k = t0 + (uint32_t)lane;
+                    const bool act = k < NE;
+                    uint64_t lo = 0, hi = 0;
+                    uint32_t a = 0, len = 0;
+                    if (act) {
+                        const bool first = k < o;   // the open token: its bytes were read at its start
+                        a = first ? ostart : c0 + S[k - o];
+                        len = c0 + E[k] - a;
+                        if (first) {
+                            lo = olo;
+                            hi = ohi;
+                        } else {
+                            window_key(L.win, a, lo, hi);
+                        }
+                        mask_key(len, lo, hi);
+                    }
+                    // (never taken -- the pairing was checked above -- but a token outside the text
+                    // must not reach the reads below: the file would go to the host instead)
+                    if (__ballot(act && (len == 0 || a >= nb || len > nb - a))) {
+                        over = true;
+                        break;
+                    }
+                    if (!(WORDS_DIAG & 1)) words += lookup_tokens(L, act, lo, hi, len, a, v, ft, fm);
+                    if (words > (uint32_t)kSetMax) over = true;
+                }
+                // the last start without an end stays open (its first 16 bytes read now, while
+                // its chunk is in the window)
+                if (NS + o == NE) {
+                    open = false;
+                } else if (NS > 0) {   // (NS == 0: the open token runs on through the chunk)
+                    open = true;
+                    ostart = rfl(c0 + (uint32_t)S[NS - 1]);
+                    window_key_u(L.win, ostart, olo, ohi);
+                }
+                prevw = wlast;   // (the block loop's view: a joined apostrophe continues the run)
+                ptail = (uint32_t)__builtin_amdgcn_readlane((int)x.w, kWave - 1);
+                asm volatile("" ::: "memory");
+                if (c + 2 < nchunks) chunk_store(c + 2, nx);   // into the slot of chunk c
+                continue;
+            }
+#endif
             for (uint32_t b0 = c * kChunk; b0 < nb && b0 < (c + 1) * kChunk && !(WORDS_DIAG & 4); b0 += kWave) {
                 const uint32_t p = b0 + (uint32_t)lane;
                 const uint32_t ch = p < nb ? L.win[p & (kWin - 1)] : 0u;
@@ -442,6 +587,10 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                 if (!(WORDS_DIAG & 2)) push(ends_here, p, len, lo, hi);
                 flush(kQKeep);   // room for the next block's tokens (at most 33)
             }
+#if !WORDS_BLOCKS_ONLY
+            flush(0);   // (the next chunk may take the fast path, which uses the queue's key area)
+            ptail = rfl(*reinterpret_cast<const uint32_t*>(L.win + ((c0 + kChunk - 4u) & (kWin - 1))));
+#endif
             if (c + 2 < nchunks) chunk_store(c + 2, nx);   // into the slot of chunk c
         }
         if (open && !over) {   // the last run reaches the end of the text
