@@ -116,6 +116,27 @@ def test_token_corner_cases(vendored):
     _check_equal(sc, hp, texts)
 
 
+def test_apostrophes_across_chunk_edges(vendored):
+    """The chunk-at-once scan joins runs over the apostrophes the regex consumes and hands chunks
+    with "'s'" (or a joining apostrophe in their last two bytes) to the block loop: every such
+    pattern placed across the 1 KiB chunk edges (and the 16-byte lane edges next to them), with
+    the chunks around it taking either path."""
+    corpus, hp, sc = vendored
+    pats = ["users'", "x's", "s's'", "a's's", "it's'", "users''s", "s'x", "'s", "x'sx", "licensor's'", "s'''s",
+            "don't", "its's's", "s's", "-'s", "/'s'"]
+    filler = 'permission is hereby granted '
+    texts = []
+    for edge in (1024, 2048):
+        for shift in range(-7, 7):
+            for pat in pats:
+                head = (filler * 100)[:edge + shift]
+                tail = " licensor's grant users' rights " + filler * 3
+                texts.append(head + pat + tail)
+                texts.append(head + pat + "'s" + pat + tail)   # the block loop's chunk, then more
+    texts += [("x's " * 300)[:k] + "s's' tail" for k in range(1010, 1030)]
+    _check_equal(sc, hp, texts)
+
+
 def test_overflowing_set_is_flagged_and_patched(vendored):
     """A file with more distinct non-vocabulary words than the device set holds is flagged
     (status 1, row left empty); dice_batch_set_rows then installs the host-prepared row."""
