@@ -72,7 +72,7 @@ __device__ __forceinline__ bool word_byte(uint32_t c) {
 }
 
 struct VocabDev {
-    const uint32_t* slots;   // [nb][8]: (tag << id_bits) | (id + 1), 0 = empty
+    const uint32_t* slots;   // [nb][kSlots]: (tag << id_bits) | (id + 1), 0 = empty
     const uint4* keys;       // [n] {lo, hi} of the word's first 16 bytes
     const uint32_t* wmeta;   // [n] length | tail hash... (see dice_vocab_setup): length
     const uint32_t* woff;    // [n] offset of the word's bytes in wtxt
@@ -149,6 +149,11 @@ __device__ inline bool bytes_equal(const uint8_t* ba, uint64_t a, const uint8_t*
     return true;
 }
 
+#ifndef WORDS_SLOTS
+#define WORDS_SLOTS 8   // tagged slots per vocabulary bucket (4: one 16-byte load, measured slower)
+#endif
+constexpr int kSlots = WORDS_SLOTS;
+
 __device__ __forceinline__ uint32_t pick8(const uint4& a, const uint4& b, int j) {   // (no indexed array)
     const uint4 q = j < 4 ? a : b;
     const int k = j & 3;
@@ -161,12 +166,12 @@ __device__ inline int32_t vocab_find(const VocabDev& v, uint64_t h, uint64_t lo,
     const uint32_t idmask = (1u << v.id_bits) - 1u;
     const uint32_t tag = ((uint32_t)(h >> 40)) << v.id_bits;
     for (uint32_t b = (uint32_t)h & v.bmask, probe = 0; probe <= v.bmask; b = (b + 1) & v.bmask, ++probe) {
-        const uint4* bk = reinterpret_cast<const uint4*>(v.slots + (size_t)b * 8);
-        const uint4 s0 = bk[0], s1 = bk[1];
+        const uint4* bk = reinterpret_cast<const uint4*>(v.slots + (size_t)b * kSlots);
+        const uint4 s0 = bk[0], s1 = kSlots == 8 ? bk[1] : make_uint4(0, 0, 0, 0);
         const uint32_t s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
         uint32_t hits = 0, empty = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < kSlots; ++j) {
             empty |= (uint32_t)(s[j] == 0) << j;
             hits |= (uint32_t)(s[j] != 0 && (s[j] & ~idmask) == tag) << j;
         }
@@ -175,8 +180,10 @@ __device__ inline int32_t vocab_find(const VocabDev& v, uint64_t h, uint64_t lo,
             hits &= hits - 1;
             const int32_t id = (int32_t)(pick8(s0, s1, j) & idmask) - 1;
             const uint4 k = v.keys[id];
+            // (a key of < 16 bytes holds a zero byte where the word ends: equal keys, equal lengths;
+            // the length is read only for 16 bytes and more)
             if (((uint64_t)k.x | ((uint64_t)k.y << 32)) == lo && ((uint64_t)k.z | ((uint64_t)k.w << 32)) == hi &&
-                v.wmeta[id] == len && (len <= 16 || bytes_equal(v.wtxt, v.woff[id], text, pos, 16, len)))
+                (len < 16 || v.wmeta[id] == len) && (len <= 16 || bytes_equal(v.wtxt, v.woff[id], text, pos, 16, len)))
                 return id;
         }
         if (empty) return -1;
@@ -711,11 +718,11 @@ int dice_vocab_setup(dice_ctx* c, int32_t n_words, const char* const* words, int
             if (ch >= 0x80) return fail(DICE_E_ARG, "words are ASCII (the wordset scan's [\\w/-])");
     }
     size_t nb = 2;
-    while (nb * 8 < 2 * (size_t)n + 1) nb <<= 1;
+    while (nb * dice::kSlots < 2 * (size_t)n + 1) nb <<= 1;
     uint32_t id_bits = 1;
     while (((uint64_t)1 << id_bits) <= (uint64_t)n + 1) ++id_bits;
     if (id_bits > 28) return fail(DICE_E_ARG, "too many words");
-    std::vector<uint32_t> slots(nb * 8, 0), wlen((size_t)n), woff((size_t)n);
+    std::vector<uint32_t> slots(nb * dice::kSlots, 0), wlen((size_t)n), woff((size_t)n);
     std::vector<uint4> keys((size_t)n);
     std::string txt;
     for (int32_t i = 0; i < n; ++i) {
@@ -729,14 +736,14 @@ int dice_vocab_setup(dice_ctx* c, int32_t n_words, const char* const* words, int
         const uint64_t h = dice::words_mix(lo, hi, wlen[(size_t)i], tail);
         const uint32_t tag = ((uint32_t)(h >> 40)) << id_bits;
         for (size_t b = h & (nb - 1);; b = (b + 1) & (nb - 1)) {
-            uint32_t* r = slots.data() + b * 8;
+            uint32_t* r = slots.data() + b * dice::kSlots;
             int j = 0;
-            while (j < 8 && r[j]) {
+            while (j < dice::kSlots && r[j]) {
                 const uint32_t id = (r[j] & ((1u << id_bits) - 1u)) - 1u;
                 if (w[id] == w[(size_t)i]) return fail(DICE_E_ARG, "duplicate word: " + w[(size_t)i]);
                 ++j;
             }
-            if (j < 8) {
+            if (j < dice::kSlots) {
                 r[j] = tag | (uint32_t)(i + 1);
                 break;
             }
