@@ -297,7 +297,12 @@ __device__ __forceinline__ void classify4(uint32_t x, uint32_t& w, uint32_t& q, 
     s = pack(eq(y ^ 0x73737373u) & ~hib);
 }
 
-__global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
+// (4 waves per SIMD asked for: the allocator then fits the kernel in 4 waves' registers with room to
+// spare; 1 = no request, for A/B: profiles/raw/r6w8_waves_per_eu_ab.txt)
+#ifndef WORDS_WAVES_PER_EU
+#define WORDS_WAVES_PER_EU 4
+#endif
+__global__ __launch_bounds__(kWordsWaves * kWave) __attribute__((amdgpu_waves_per_eu(WORDS_WAVES_PER_EU))) void dice_words_kernel(
     const uint8_t* __restrict__ text, int64_t text_bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ tlen, int64_t n, VocabDev v, int32_t w64, uint64_t* __restrict__ rows,
     uint32_t* __restrict__ wf_out, uint64_t* __restrict__ fmask_out, uint8_t* __restrict__ status,
@@ -448,23 +453,24 @@ __global__ __launch_bounds__(kWordsWaves * kWave) void dice_words_kernel(
                     E[k] = (uint16_t)(16u * (uint32_t)lane + (uint32_t)__builtin_ctz(m));
                 asm volatile("" ::: "memory");
                 const uint32_t o = open ? 1u : 0u;
+                auto token = [&](uint32_t k, uint64_t& lo, uint64_t& hi, uint32_t& a, uint32_t& len) {
+                    const bool first = k < o;   // the open token: its bytes were read at its start
+                    a = first ? ostart : c0 + S[k - o];
+                    len = c0 + E[k] - a;
+                    if (first) {
+                        lo = olo;
+                        hi = ohi;
+                    } else {
+                        window_key(L.win, a, lo, hi);
+                    }
+                    mask_key(len, lo, hi);
+                };
                 for (uint32_t t0 = 0; t0 < NE && !over; t0 += kWave) {
                     const uint32_t k = t0 + (uint32_t)lane;
                     const bool act = k < NE;
                     uint64_t lo = 0, hi = 0;
                     uint32_t a = 0, len = 0;
-                    if (act) {
-                        const bool first = k < o;   // the open token: its bytes were read at its start
-                        a = first ? ostart : c0 + S[k - o];
-                        len = c0 + E[k] - a;
-                        if (first) {
-                            lo = olo;
-                            hi = ohi;
-                        } else {
-                            window_key(L.win, a, lo, hi);
-                        }
-                        mask_key(len, lo, hi);
-                    }
+                    if (act) token(k, lo, hi, a, len);
                     // (never taken -- the pairing was checked above -- but a token outside the text
                     // must not reach the reads below: the file would go to the host instead)
                     if (__ballot(act && (len == 0 || a >= nb || len > nb - a))) {
