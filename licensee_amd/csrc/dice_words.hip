@@ -11,20 +11,21 @@
 //
 // One wave per file, persistent over the batch. The file streams through a per-wave LDS window of
 // two 1 KiB chunks (one 16-byte load per lane, the chunk after next in flight while this one is
-// scanned). A 64-byte block is one byte per lane: a ballot of the [\w/-] class gives the block's
-// word mask, and, as in the host scan (normalize.cpp scan_words), a token is a run of it -- its
-// start lane finds its end in the mask; the last run of a block stays open into the next -- except
-// that a run followed by an apostrophe is re-scanned by the regex's own loop ('s and s' continue a
-// token): a block with such a run is scanned serially (rare). A token's first 16 bytes, read from
-// the window at its start, are its key (with its length and, past 16 bytes, a hash of the tail);
-// keys queue in LDS and are looked up 64 at a time (lanes = tokens) in the context's vocabulary
-// table (L2-resident, dice_vocab_setup: buckets of 8 tagged slots, the full key checked, long
-// words' tails compared byte by byte): a vocabulary word sets its row bit (ds_or), one of the
-// extra words (template field words outside the vocabulary) its field-mask bit, any other word
-// goes to the wave's LDS set of distinct words (CAS-claimed slots, full keys, long tokens'
-// bytes compared). |W_F| = row bits + field bits + set size. A file whose set would pass
-// kSetMax distinct non-vocabulary words is flagged; the caller prepares it on the host.
-// LDS ~10 KiB per wave at the vendored vocabulary: four 4-wave workgroups per CU.
+// scanned). Most chunks are scanned at once: each lane classifies its 16 bytes and the 4 on either
+// side with SWAR, the regex's tokens are the runs of [\w/-] joined by the apostrophes it consumes,
+// and the k-th run end closes the k-th run start (the token open from the previous chunk first).
+// A chunk where that joining rule is not exact ("'s'"), or that a serial re-scan reached into,
+// takes the block loop: 64-byte blocks, one byte per lane, a ballot word mask (as in the host scan,
+// normalize.cpp scan_words), and a block with a run ending at an apostrophe next to an 's' scanned
+// serially in the regex's own order. A token's first 16 bytes, read from the window, are its key
+// (with its length and, past 16 bytes, a hash of the tail); tokens are looked up 64 at a time
+// (lanes = tokens) in the context's vocabulary table (L2-resident, dice_vocab_setup: buckets of 8
+// tagged slots, the full key checked, long words' tails compared byte by byte): a vocabulary word
+// sets its row bit (ds_or), one of the extra words (template field words outside the vocabulary)
+// its field-mask bit, any other word goes to the wave's LDS set of distinct words (CAS-claimed
+// slots, full keys, long tokens' bytes compared). |W_F| = row bits + field bits + set size. A
+// file whose set would pass kSetMax distinct non-vocabulary words is flagged; the caller prepares
+// it on the host. LDS ~10 KiB per wave at the vendored vocabulary: four 4-wave workgroups per CU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
