@@ -1,4 +1,4 @@
-"""Register budgets of the T > 64 kernels, from the compiler's resource remarks (no GPU needed).
+"""Register budgets of the T > 64 kernels and the wordset scan, from the compiler's resource remarks (no GPU needed).
 
 The postings kernels and the config-3 pruned kernel are written for 8 waves per SIMD (64 VGPRs,
 two 16-wave workgroups per CU). A kernel that spills to scratch pays a reload whose vmcnt(0) waits
@@ -53,3 +53,13 @@ def test_mfma_dense_prefix_kernel_fits_3_waves_without_scratch():
         r = next(v for k, v in res.items() if k.endswith('dice::' + name))
         assert r['ScratchSize [bytes/lane]'] == '0' and r['VGPRs Spill'] == '0', (name, r)
         assert int(r['Occupancy [waves/SIMD]']) >= 3, (name, r)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not present')
+def test_wordset_scan_kernel_fits_4_waves_without_scratch():
+    """dice_words_kernel: 4-wave workgroups, four per CU (LDS ~10 KiB per wave), asked for 4 waves
+    per SIMD (amdgpu_waves_per_eu) -- no scratch, VGPRs within 4 waves' share."""
+    res = _resources('dice_words.hip')
+    r = next(v for k, v in res.items() if k.endswith('dice::dice_words_kernel'))
+    assert r['ScratchSize [bytes/lane]'] == '0' and r['VGPRs Spill'] == '0', r
+    assert int(r['Occupancy [waves/SIMD]']) >= 4, r
