@@ -55,6 +55,9 @@ constexpr int kQCap = kQKeep + 33;      // + one block's tokens (32 runs + the o
 constexpr uint64_t kLongMark = 1ull << 63;   // set key of a token longer than 16 bytes
 constexpr uint32_t kFastPos = kQCap * 16 / 2;   // run starts + ends of a fast-path chunk (u16 each in
                                                 // the queue's qlo + qhi area)
+#ifndef WORDS_DYNAMIC
+#define WORDS_DYNAMIC 1   // 0: files by a fixed stride of the grid (A/B)
+#endif
 #ifndef WORDS_BLOCKS_ONLY
 #define WORDS_BLOCKS_ONLY 0   // 1: every chunk through the block loop (A/B: tools/build_variant.sh)
 #endif
@@ -323,7 +326,19 @@ __global__ __launch_bounds__(kWordsWaves * kWave) __attribute__((amdgpu_waves_pe
     L.so = reinterpret_cast<uint32_t*>(L.qmeta + kQCap);
     L.row = L.so + kSetCap;
 
+#if WORDS_DYNAMIC
+    // files handed out one at a time from a counter (counters[2], zeroed per upload): a wave's share
+    // is then not a fixed stride of files whose sizes vary several-fold (the slowest wave's sum
+    // set the kernel's end): 1.83 vs 2.51 ms per 64k texts, profiles/raw/r6w9_dynamic_ab.txt
+    for (;;) {
+        // (every lane takes part -- lane 0 adds 1, the rest 0 -- so no lane's result comes from a
+        // divergent branch; lane 0's old value is the file)
+        const uint32_t got = atomicAdd(counters + 2, lane == 0 ? 1u : 0u);
+        const int64_t f = (int64_t)(uint32_t)__shfl((int)got, 0);
+        if (f >= n) break;
+#else
     for (int64_t f = (int64_t)blockIdx.x * kWordsWaves + wave; f < n; f += (int64_t)gridDim.x * kWordsWaves) {
+#endif
         // (uniform values read from memory go through readfirstlane: the state below that derives
         // from them -- masks, resume, the open token -- then stays scalar instead of being carried
         // per lane with exec-masked branches)
@@ -793,7 +808,7 @@ int dice_batch_upload_text(dice_batch* b, int64_t n, const uint8_t* text, int64_
     dice::WGuard g(c->device);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int rc;
-    size_t cap8 = (size_t)b->capacity * 8, cap4 = (size_t)b->capacity * 4, cap1 = (size_t)b->capacity, capc = 8;
+    size_t cap8 = (size_t)b->capacity * 8, cap4 = (size_t)b->capacity * 4, cap1 = (size_t)b->capacity, capc = 16;
     size_t tneed = (size_t)text_bytes + 64;   // (load32's slack past the last token)
     if (tneed > b->text_cap) {
         if (hipStreamSynchronize(s) != hipSuccess) return fail(DICE_E_DEVICE, "hipStreamSynchronize failed");
@@ -812,7 +827,7 @@ int dice_batch_upload_text(dice_batch* b, int64_t n, const uint8_t* text, int64_
     if (hipMemcpyAsync(b->d_text, text, (size_t)text_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(b->d_toff, offsets, (size_t)n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(b->d_tlen, text_len, (size_t)n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(b->d_wcnt, 0, 8, s) != hipSuccess)
+        hipMemsetAsync(b->d_wcnt, 0, 16, s) != hipSuccess)   // (overflow, long, next file)
         return fail(DICE_E_DEVICE, "text upload failed");
     dice::VocabDev v;
     v.slots = (const uint32_t*)c->d_wslots;
